@@ -1,0 +1,169 @@
+"""ctypes loader for the CPU oracle (oracle/liboracle.so).
+
+Test infrastructure only: the oracle is the checker for parity tests and the
+CPU baseline in bench.py; the product (libcda) never loads it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+_LIB = None
+
+SHARE = 512
+NS = 29
+NODE = 90
+
+OK, E_NOT_POW2, E_NOT_SQUARE, E_SHARD_SIZE, E_NS_SHORT, E_NS_ORDER, E_TOO_FEW, \
+    E_UNREPAIRABLE, E_BYZANTINE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(ORACLE_DIR, "liboracle.so")
+        if not os.path.exists(path):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        L.ora_sha256.argtypes = [P, ctypes.c_size_t, P]
+        L.ora_leo_bits_for.argtypes = [ctypes.c_int]
+        L.ora_leo_encode.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P]
+        L.ora_leo_decode.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P]
+        L.ora_leo_mul.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_uint]
+        L.ora_leo_mul.restype = ctypes.c_uint
+        L.ora_leo_skew.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.ora_leo_log.argtypes = [ctypes.c_int, ctypes.c_uint]
+        L.ora_leo_exp.argtypes = [ctypes.c_int, ctypes.c_uint]
+        L.ora_nmt_axis_root.argtypes = [ctypes.c_uint64, ctypes.c_uint64, P, P, ctypes.c_int, P, P]
+        L.ora_merkle_root.argtypes = [P, P, ctypes.c_int, P]
+        L.ora_extend.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, ctypes.c_int]
+        L.ora_roots.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, ctypes.c_int, P, P]
+        L.ora_dah_hash.argtypes = [ctypes.c_int, P, P, P]
+        L.ora_extend_commit.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, ctypes.c_int]
+        L.ora_repair.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, P]
+        L.ora_gen_ods.argtypes = [ctypes.c_int, ctypes.c_uint64, P]
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _ptr_array(rows):
+    arr = (ctypes.c_void_p * len(rows))()
+    for i, r in enumerate(rows):
+        arr[i] = r.ctypes.data
+    return arr
+
+
+def sha256(b: bytes) -> bytes:
+    out = np.zeros(32, np.uint8)
+    buf = np.frombuffer(b, np.uint8).copy() if b else np.zeros(1, np.uint8)
+    lib().ora_sha256(_p(buf), len(b), _p(out))
+    return out.tobytes()
+
+
+def gen_ods(k: int, seed: int) -> np.ndarray:
+    """Namespace-sorted synthetic ODS (k*k, 512) — SURVEY §8d generator."""
+    ods = np.zeros((k * k, SHARE), np.uint8)
+    lib().ora_gen_ods(k, seed, _p(ods))
+    return ods
+
+
+def leo_encode(data: np.ndarray) -> np.ndarray:
+    """data: (k, L) uint8 -> parity (k, L)."""
+    data = np.ascontiguousarray(data, np.uint8)
+    k, L = data.shape
+    par = np.zeros_like(data)
+    rows_d = [data[i] for i in range(k)]
+    rows_p = [par[i] for i in range(k)]
+    rc = lib().ora_leo_encode(k, L, _ptr_array(rows_d), _ptr_array(rows_p))
+    if rc != 0:
+        raise ValueError(f"ora_leo_encode rc={rc}")
+    return par
+
+
+def leo_decode(shards: np.ndarray, present: np.ndarray):
+    """shards: (2k, L) with garbage where missing; returns (rc, repaired copy)."""
+    sh = np.ascontiguousarray(shards, np.uint8).copy()
+    n, L = sh.shape
+    pres = np.ascontiguousarray(present, np.uint8)
+    rows = [sh[i] for i in range(n)]
+    rc = lib().ora_leo_decode(n // 2, L, _ptr_array(rows), _p(pres))
+    return rc, sh
+
+
+def extend(ods: np.ndarray, nthreads: int = 8) -> np.ndarray:
+    n = ods.shape[0]
+    k = int(round(n ** 0.5))
+    L = ods.shape[1]
+    eds = np.zeros((4 * k * k, L), np.uint8)
+    lib().ora_extend(k, L, _p(np.ascontiguousarray(ods)), _p(eds), nthreads)
+    return eds
+
+
+def roots(eds: np.ndarray, nthreads: int = 8):
+    n = eds.shape[0]
+    w = int(round(n ** 0.5))
+    k = w // 2
+    rr = np.zeros((w, NODE), np.uint8)
+    cr = np.zeros((w, NODE), np.uint8)
+    ea = np.zeros(1, np.int32)
+    ei = np.zeros(1, np.int32)
+    rc = lib().ora_roots(k, eds.shape[1], _p(np.ascontiguousarray(eds)), _p(rr), _p(cr), nthreads, _p(ea), _p(ei))
+    return rc, rr, cr, int(ea[0]), int(ei[0])
+
+
+def dah_hash(row_roots: np.ndarray, col_roots: np.ndarray) -> bytes:
+    out = np.zeros(32, np.uint8)
+    lib().ora_dah_hash(row_roots.shape[0], _p(np.ascontiguousarray(row_roots)),
+                       _p(np.ascontiguousarray(col_roots)), _p(out))
+    return out.tobytes()
+
+
+def extend_commit(shares: np.ndarray, want_eds: bool = True, nthreads: int = 8):
+    """da.ExtendShares + NewDataAvailabilityHeader. Returns (rc, eds, row_roots, col_roots, dah)."""
+    shares = np.ascontiguousarray(shares, np.uint8)
+    count, L = shares.shape
+    k = max(1, int(round(count ** 0.5)))
+    eds = np.zeros((4 * k * k, L), np.uint8) if want_eds else None
+    rr = np.zeros((2 * k, NODE), np.uint8)
+    cr = np.zeros((2 * k, NODE), np.uint8)
+    dah = np.zeros(32, np.uint8)
+    rc = lib().ora_extend_commit(count, L, _p(shares), _p(eds) if eds is not None else None,
+                                 _p(rr), _p(cr), _p(dah), nthreads)
+    return rc, eds, rr, cr, dah.tobytes()
+
+
+def nmt_axis_root(square_size: int, axis_index: int, leaves):
+    arrs = [np.frombuffer(bytes(l), np.uint8).copy() if len(l) else np.zeros(1, np.uint8) for l in leaves]
+    lens = np.array([len(l) for l in leaves], np.uint64) if leaves else np.zeros(1, np.uint64)
+    root = np.zeros(NODE, np.uint8)
+    err = np.zeros(1, np.int32)
+    rc = lib().ora_nmt_axis_root(square_size, axis_index, _ptr_array(arrs) if arrs else None,
+                                 _p(lens), len(leaves), _p(root), _p(err))
+    return rc, root.tobytes(), int(err[0])
+
+
+def merkle_root(items) -> bytes:
+    arrs = [np.frombuffer(bytes(i), np.uint8).copy() if len(i) else np.zeros(1, np.uint8) for i in items]
+    lens = np.array([len(i) for i in items], np.uint64) if items else np.zeros(1, np.uint64)
+    out = np.zeros(32, np.uint8)
+    lib().ora_merkle_root(_ptr_array(arrs) if arrs else None, _p(lens), len(items), _p(out))
+    return out.tobytes()
+
+
+def repair(eds: np.ndarray, present: np.ndarray, row_roots: np.ndarray, col_roots: np.ndarray):
+    eds = np.ascontiguousarray(eds, np.uint8).copy()
+    pres = np.ascontiguousarray(present, np.uint8).copy()
+    w = row_roots.shape[0]
+    ea = np.zeros(1, np.int32)
+    ei = np.zeros(1, np.int32)
+    rc = lib().ora_repair(w // 2, eds.shape[1], _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots)),
+                          _p(np.ascontiguousarray(col_roots)), _p(ea), _p(ei))
+    return rc, eds, pres, int(ea[0]), int(ei[0])
