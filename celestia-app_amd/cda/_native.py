@@ -1,0 +1,268 @@
+"""ctypes binding of libcda.so (include/cda.h).
+
+The product path: every compute call goes through the HIP library.  There is
+no CPU fallback — if libcda.so is missing or no GPU is visible the calls raise.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcda.so")
+
+SHARE_SIZE = 512
+NAMESPACE_SIZE = 29
+NODE_SIZE = 90
+HASH_SIZE = 32
+REC_BYTES = 96
+
+OK = 0
+E_NOT_POW2 = -1
+E_NOT_SQUARE = -2
+E_SHARD_SIZE = -3
+E_NS_SHORT = -4
+E_NS_ORDER = -5
+E_TOO_FEW = -6
+E_UNREPAIRABLE = -7
+E_BYZANTINE = -8
+E_ARG = -9
+E_DEVICE = -10
+E_PUSH_PAST = -11
+E_UNSUPPORTED = -12
+
+AXIS_ROW = 0
+AXIS_COL = 1
+
+# Every symbol declared in include/cda.h (checked by tests/test_abi.py).
+EXPORTS = [
+    "cda_init", "cda_free", "cda_strerror", "cda_last_device_error",
+    "cda_rs_encode", "cda_rs_decode", "cda_rs_max_chunks", "cda_rs_name", "cda_rs_validate_chunk_size",
+    "cda_extend_commit", "cda_extend_commit_batch", "cda_extend_commit_device", "cda_commit_eds",
+    "cda_dah_hash", "cda_nmt_axis_root", "cda_repair",
+    "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
+]
+
+
+class ErrInfo(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("axis", ctypes.c_int32), ("index", ctypes.c_int32),
+                ("leaf", ctypes.c_int32), ("block", ctypes.c_int32)]
+
+
+class CdaError(Exception):
+    """Error returned by libcda; `code` is a CDA_E_* value."""
+
+    def __init__(self, code, msg="", axis=-1, index=-1, leaf=-1, block=-1):
+        self.code, self.axis, self.index, self.leaf, self.block = code, axis, index, leaf, block
+        super().__init__(f"{msg or strerror(code)} (code {code}, axis {axis}, index {index}, leaf {leaf})")
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib():
+    """Load libcda.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libcda.so not built at {LIB_PATH}; run __graft_entry__.build()")
+            L = ctypes.CDLL(LIB_PATH)
+            P, U32, I32, U64, I64, SZ = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64,
+                                          ctypes.c_int64, ctypes.c_size_t)
+            sig = {
+                "cda_init": (I32, [I32, ctypes.POINTER(P)]),
+                "cda_free": (None, [P]),
+                "cda_strerror": (ctypes.c_char_p, [I32]),
+                "cda_last_device_error": (ctypes.c_char_p, [P]),
+                "cda_rs_encode": (I32, [P, U32, U32, P, P]),
+                "cda_rs_decode": (I32, [P, U32, U32, P, P]),
+                "cda_rs_max_chunks": (I64, []),
+                "cda_rs_name": (ctypes.c_char_p, []),
+                "cda_rs_validate_chunk_size": (I32, [I64]),
+                "cda_extend_commit": (I32, [P, U32, U32, P, P, P, P, P, P]),
+                "cda_extend_commit_batch": (I32, [P, U32, U32, P, P, P, P, P, P]),
+                "cda_extend_commit_device": (I32, [P, U32, U32, P, P, P, P, P, P]),
+                "cda_commit_eds": (I32, [P, U32, P, P, P, P, P]),
+                "cda_dah_hash": (I32, [P, U32, P, P, P]),
+                "cda_nmt_axis_root": (I32, [P, U64, U64, U32, U32, P, P, P]),
+                "cda_repair": (I32, [P, U32, P, P, P, P, P]),
+                "cda_profile_enable": (I32, [P, I32]),
+                "cda_profile_read": (I32, [P, P, SZ, P, P, I32]),
+                "cda_profile_reset": (I32, [P]),
+            }
+            for name, (res, args) in sig.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def strerror(code):
+    return lib().cda_strerror(code).decode()
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(rc, err=None, ctx=None):
+    if rc == OK:
+        return
+    if rc == E_DEVICE and ctx is not None:
+        raise CdaError(rc, "device error: " + lib().cda_last_device_error(ctx._h).decode())
+    if err is not None:
+        raise CdaError(rc, axis=err.axis, index=err.index, leaf=err.leaf, block=err.block)
+    raise CdaError(rc)
+
+
+class Context:
+    """One cda_ctx bound to one HIP device (one process per GPU)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        rc = lib().cda_init(device, ctypes.byref(h))
+        if rc != OK:
+            raise CdaError(rc, "cda_init failed (no GPU visible?)")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().cda_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- codec ----
+    def rs_encode(self, data):
+        data = np.ascontiguousarray(data, np.uint8)
+        k, L = data.shape
+        parity = np.empty_like(data)
+        _check(lib().cda_rs_encode(self._h, k, L, _p(data), _p(parity)), ctx=self)
+        return parity
+
+    def rs_decode(self, shards, present):
+        sh = np.ascontiguousarray(shards, np.uint8).copy()
+        pres = np.ascontiguousarray(present, np.uint8)
+        n, L = sh.shape
+        _check(lib().cda_rs_decode(self._h, n // 2, L, _p(sh), _p(pres)), ctx=self)
+        return sh
+
+    # ---- block path ----
+    def extend_commit(self, shares, want_eds=True):
+        shares = np.ascontiguousarray(shares, np.uint8)
+        count, L = shares.shape
+        k = max(1, int(round(count ** 0.5)))
+        eds = np.empty((4 * k * k, L), np.uint8) if want_eds else None
+        rr = np.empty((2 * k, NODE_SIZE), np.uint8)
+        cr = np.empty((2 * k, NODE_SIZE), np.uint8)
+        dah = np.empty(32, np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_extend_commit(self._h, count, L, _p(shares), _p(eds), _p(rr), _p(cr), _p(dah),
+                                     ctypes.byref(err))
+        _check(rc, err, self)
+        return eds, rr, cr, dah.tobytes()
+
+    def extend_commit_batch(self, ods, want_eds=True):
+        """ods: (nblocks, k*k, 512)."""
+        ods = np.ascontiguousarray(ods, np.uint8)
+        nb, kk, L = ods.shape
+        k = int(round(kk ** 0.5))
+        eds = np.empty((nb, 4 * k * k, L), np.uint8) if want_eds else None
+        rr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
+        cr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
+        dah = np.empty((nb, 32), np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_extend_commit_batch(self._h, k, nb, _p(ods), _p(eds), _p(rr), _p(cr), _p(dah),
+                                           ctypes.byref(err))
+        _check(rc, err, self)
+        return eds, rr, cr, dah
+
+    def extend_commit_device(self, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, stream=None):
+        rc = lib().cda_extend_commit_device(self._h, k, nblocks, ctypes.c_void_p(d_ods), ctypes.c_void_p(d_eds),
+                                            ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
+                                            ctypes.c_void_p(d_status), ctypes.c_void_p(stream or 0))
+        _check(rc, ctx=self)
+
+    def commit_eds(self, eds):
+        eds = np.ascontiguousarray(eds, np.uint8)
+        w = int(round(eds.shape[0] ** 0.5))
+        rr = np.empty((w, NODE_SIZE), np.uint8)
+        cr = np.empty((w, NODE_SIZE), np.uint8)
+        dah = np.empty(32, np.uint8)
+        err = ErrInfo()
+        _check(lib().cda_commit_eds(self._h, w // 2, _p(eds), _p(rr), _p(cr), _p(dah), ctypes.byref(err)), err, self)
+        return rr, cr, dah.tobytes()
+
+    def dah_hash(self, row_roots, col_roots):
+        n = 0 if row_roots is None else len(row_roots)
+        rr = np.ascontiguousarray(np.asarray(row_roots, np.uint8).reshape(n, NODE_SIZE)) if n else None
+        cr = np.ascontiguousarray(np.asarray(col_roots, np.uint8).reshape(n, NODE_SIZE)) if n else None
+        out = np.empty(32, np.uint8)
+        _check(lib().cda_dah_hash(self._h, n, _p(rr), _p(cr), _p(out)), ctx=self)
+        return out.tobytes()
+
+    def nmt_axis_root(self, square_size, axis_index, leaves):
+        n = len(leaves)
+        if n:
+            lens = {len(x) for x in leaves}
+            leaf_len = min(lens)
+            if len(lens) != 1:
+                raise CdaError(E_SHARD_SIZE, "leaves of unequal length")
+            buf = np.frombuffer(b"".join(bytes(x) for x in leaves), np.uint8).copy()
+        else:
+            leaf_len, buf = 0, None
+        root = np.empty(NODE_SIZE, np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_nmt_axis_root(self._h, square_size, axis_index, n, leaf_len, _p(buf), _p(root),
+                                     ctypes.byref(err))
+        _check(rc, err, self)
+        return root.tobytes()
+
+    def repair(self, eds, present, row_roots, col_roots):
+        eds = np.ascontiguousarray(eds, np.uint8).copy()
+        pres = np.ascontiguousarray(present, np.uint8).copy()
+        w = len(row_roots)
+        err = ErrInfo()
+        rc = lib().cda_repair(self._h, w // 2, _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots, np.uint8)),
+                              _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err))
+        _check(rc, err, self)
+        return eds, pres
+
+    # ---- profiling ----
+    def profile_enable(self, on=True):
+        _check(lib().cda_profile_enable(self._h, 1 if on else 0), ctx=self)
+
+    def profile_reset(self):
+        _check(lib().cda_profile_reset(self._h), ctx=self)
+
+    def profile_read(self):
+        cap = 64
+        names = ctypes.create_string_buffer(4096)
+        ms = np.zeros(cap, np.float64)
+        cnt = np.zeros(cap, np.int64)
+        n = lib().cda_profile_read(self._h, names, 4096, _p(ms), _p(cnt), cap)
+        out, parts = {}, names.raw.split(b"\0")
+        for i in range(n):
+            out[parts[i].decode()] = (float(ms[i]), int(cnt[i]))
+        return out
+
+
+_default = None
+_default_lock = threading.Lock()
+
+
+def default_context():
+    global _default
+    with _default_lock:
+        if _default is None:
+            _default = Context(int(os.environ.get("LOCAL_RANK", "0")) if os.environ.get("CDA_USE_LOCAL_RANK") else 0)
+    return _default

@@ -1,0 +1,113 @@
+"""pkg/da mirror (pkg/da/data_availability_header.go, celestia-app @ 2025-02-13)."""
+import math
+
+import numpy as np
+
+from . import _native as N
+from . import appconsts
+from .rsmt2d import ExtendedDataSquare, LeoRSCodec
+
+MAX_EXTENDED_SQUARE_WIDTH = appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND * 2
+MIN_EXTENDED_SQUARE_WIDTH = appconsts.MIN_SQUARE_SIZE * 2
+
+
+class DAError(Exception):
+    pass
+
+
+def round_up_power_of_two(x):
+    r = 1
+    while r < x:
+        r <<= 1
+    return r
+
+
+def square_size(n):
+    """SquareSize(len) = RoundUpPowerOfTwo(ceil(sqrt(len)))  (:205-207)."""
+    return round_up_power_of_two(int(math.ceil(math.sqrt(n))))
+
+
+def is_power_of_two(n):
+    return n > 0 and (n & (n - 1)) == 0
+
+
+def extend_shares(shares, codec=None):
+    """ExtendShares (:65-75)."""
+    if not is_power_of_two(len(shares)):
+        raise DAError(f"number of shares is not a power of 2: got {len(shares)}")
+    codec = codec or LeoRSCodec()
+    arr = np.stack([np.frombuffer(bytes(s), np.uint8) for s in shares])
+    eds, rr, cr, _ = codec.ctx.extend_commit(arr)
+    k = int(round(len(shares) ** 0.5))
+    return ExtendedDataSquare(eds, 2 * k, k, codec, rr, cr)
+
+
+class DataAvailabilityHeader:
+    def __init__(self, row_roots=None, column_roots=None, ctx=None):
+        self.row_roots = [bytes(r) for r in (row_roots or [])]
+        self.column_roots = [bytes(r) for r in (column_roots or [])]
+        self._hash = b""
+        self._ctx = ctx
+
+    def hash(self):
+        """Hash (:92-108): RFC-6962 root of rowRoots ‖ columnRoots (memoised)."""
+        if self._hash:
+            return self._hash
+        ctx = self._ctx or N.default_context()
+        n = len(self.row_roots)
+        if n == 0 and len(self.column_roots) == 0:
+            self._hash = ctx.dah_hash(None, None)
+        else:
+            self._hash = ctx.dah_hash(np.frombuffer(b"".join(self.row_roots), np.uint8).reshape(n, -1),
+                                      np.frombuffer(b"".join(self.column_roots), np.uint8).reshape(n, -1))
+        return self._hash
+
+    def string(self):
+        return self.hash().hex().upper()
+
+    def equals(self, other):
+        return self.hash() == other.hash()
+
+    def is_zero(self):
+        return len(self.column_roots) == 0 or len(self.row_roots) == 0
+
+    def square_size(self):
+        return len(self.row_roots) // 2
+
+    def validate_basic(self):
+        """ValidateBasic (:134-162)."""
+        if len(self.column_roots) < MIN_EXTENDED_SQUARE_WIDTH or len(self.row_roots) < MIN_EXTENDED_SQUARE_WIDTH:
+            raise DAError(f"minimum valid DataAvailabilityHeader has at least {MIN_EXTENDED_SQUARE_WIDTH} "
+                          "row and column roots")
+        if len(self.column_roots) > MAX_EXTENDED_SQUARE_WIDTH or len(self.row_roots) > MAX_EXTENDED_SQUARE_WIDTH:
+            raise DAError(f"maximum valid DataAvailabilityHeader has at most {MAX_EXTENDED_SQUARE_WIDTH} "
+                          "row and column roots")
+        if len(self.column_roots) != len(self.row_roots):
+            raise DAError(f"unequal number of row and column roots: row {len(self.row_roots)} "
+                          f"col {len(self.column_roots)}")
+        if len(self.hash()) != appconsts.HASH_LENGTH:
+            raise DAError("wrong hash: expected size to be 32 bytes")
+
+
+def new_data_availability_header(eds: ExtendedDataSquare):
+    """NewDataAvailabilityHeader (:44-63)."""
+    dah = DataAvailabilityHeader(eds.row_roots(), eds.col_roots(), ctx=eds.codec.ctx)
+    dah.hash()
+    return dah
+
+
+def tail_padding_share():
+    """go-square shares.TailPaddingShare: ns ‖ info(0x01) ‖ seqlen 0 ‖ zeros (specs shares.md:71-81)."""
+    s = bytearray(appconsts.SHARE_SIZE)
+    s[:29] = appconsts.TAIL_PADDING_NAMESPACE
+    s[29] = 0x01
+    return bytes(s)
+
+
+def min_shares():
+    return [tail_padding_share()]
+
+
+def min_data_availability_header():
+    """MinDataAvailabilityHeader (:179-190)."""
+    return new_data_availability_header(extend_shares(min_shares()))

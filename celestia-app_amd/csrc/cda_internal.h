@@ -1,0 +1,67 @@
+// cda_internal.h — internal declarations shared by the HIP kernels and the host engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/cda.h"
+
+#define CDA_SHARE 512
+#define CDA_REC_WORDS 24 /* 96-byte node record: 90-byte NMT node + 6 zero bytes */
+#define CDA_REC_BYTES 96
+
+namespace cda {
+
+// Leopard field tables (product-side; built in leopard_tables.cpp).
+struct LeoTables {
+  int bits;
+  unsigned order, modulus;
+  const uint16_t* exp_t;  // [order]
+  const uint16_t* log_t;  // [order]
+  const uint16_t* skew;   // [modulus]
+};
+const LeoTables& leo_tables(int bits);
+// 64-bit bit-matrix of "multiply by exp(log_m)" in GF(2^8) (Leopard representation):
+// byte b = (1 << b) * exp(log_m).  log_m == 255 -> all zero (multiplier 0).
+uint64_t leo8_colbits(unsigned log_m);
+// 16 x 16 bit-matrix for GF(2^16): word b (uint16) = (1 << b) * exp(log_m).
+void leo16_colbits(unsigned log_m, uint16_t out[16]);
+
+// Description of one batched codeword encode launch (byte strides).
+struct RsJob {
+  const uint8_t* src;
+  long long src_blk, src_cw, src_sh;
+  uint8_t* dst;
+  long long dst_blk, dst_cw, dst_sh;
+  uint8_t* cpy;  // optional copy of the data shards (may be null)
+  long long cpy_blk, cpy_cw, cpy_sh;
+  int k;           // data shards per codeword
+  int cw_per_blk;  // codewords per block
+  int nblk;        // blocks
+  int shard_len;   // bytes, multiple of 64
+};
+
+// launchers (return 0 on success, -1 on launch error)
+int rs_init_device_tables(int device);
+int launch_rs_encode8(const RsJob& job, hipStream_t s);
+int launch_rs_encode16(const RsJob& job, hipStream_t s);
+int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
+                     hipStream_t s);
+int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int nblocks, int level, hipStream_t s);
+int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s);
+// single-axis tree (wrapper.NewConstructor tree of n leaves of 512 B)
+int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,
+                     unsigned long long* d_status, hipStream_t s);
+int launch_level_generic(const void* d_in, void* d_out, int n_in, hipStream_t s);
+
+// profiling hook implemented by the engine
+struct ProfScope {
+  void* ctx;
+  const char* name;
+  hipStream_t stream;
+  hipEvent_t a, b;
+  ProfScope(void* ctx, const char* name, hipStream_t s);
+  ~ProfScope();
+};
+
+}  // namespace cda

@@ -1,0 +1,556 @@
+// engine.cpp — host side of libcda: context, device workspace, launch
+// orchestration and the C ABI declared in include/cda.h.
+//
+// The block pipeline (da.ExtendShares + da.NewDataAvailabilityHeader,
+// pkg/da/data_availability_header.go:44-75) on one HIP stream:
+//   1. rs_encode8  rows     : ODS row r -> EDS Q0 copy + Q1 row r          (k codewords / block)
+//   2. rs_encode8  columns  : EDS column c of [Q0|Q1] -> [Q2|Q3] column c  (2k codewords / block)
+//      (Q3 = Enc(Q2 rows) in rsmt2d; by linearity Enc_col(Q1) is the same bytes)
+//   3. leaf_hash            : every EDS cell once -> 96-B leaf records + namespace-order status
+//   4. nmt_level x log2(2k) : row and column trees of every block, one launch per level
+//   5. dah                  : RFC-6962 over row roots ‖ col roots
+// Nothing here computes on the CPU: the host only validates arguments, moves
+// buffers and maps device status words to error codes.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cda_internal.h"
+
+struct cda_ctx {
+  int device = 0;
+  std::recursive_mutex mu;
+  hipStream_t stream = nullptr;
+  std::string last_err;
+  // workspace
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Buf ods, eds, leaf, scratch, roots, dah, status, host_status;
+  // profiling
+  bool prof = false;
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  std::map<std::string, std::pair<double, long long>> prof_acc;
+};
+
+namespace cda {
+
+ProfScope::ProfScope(void* c, const char* n, hipStream_t s) : ctx(c), name(n), stream(s), a(nullptr), b(nullptr) {
+  cda_ctx* x = static_cast<cda_ctx*>(ctx);
+  if (!x || !x->prof) return;
+  auto get = [&]() {
+    hipEvent_t e;
+    if (!x->event_pool.empty()) {
+      e = x->event_pool.back();
+      x->event_pool.pop_back();
+    } else {
+      (void)hipEventCreate(&e);
+    }
+    return e;
+  };
+  a = get();
+  b = get();
+  (void)hipEventRecord(a, stream);
+}
+
+ProfScope::~ProfScope() {
+  cda_ctx* x = static_cast<cda_ctx*>(ctx);
+  if (!x || !x->prof || !a) return;
+  (void)hipEventRecord(b, stream);
+  x->pending.push_back({name, a, b});
+}
+
+}  // namespace cda
+
+using namespace cda;
+
+namespace {
+
+bool dev_ok(cda_ctx* c, hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  c->last_err = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+int ensure(cda_ctx* c, cda_ctx::Buf& b, size_t bytes) {
+  if (b.cap >= bytes) return CDA_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  if (!dev_ok(c, hipMalloc(&b.p, bytes ? bytes : 16), "hipMalloc")) return CDA_E_DEVICE;
+  b.cap = bytes;
+  return CDA_OK;
+}
+
+void flush_profile(cda_ctx* c) {
+  for (auto& p : c->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      auto& acc = c->prof_acc[p.name];
+      acc.first += ms;
+      acc.second += 1;
+    }
+    c->event_pool.push_back(p.a);
+    c->event_pool.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+int ilog2i(uint32_t v) {
+  int l = 0;
+  while ((1u << l) < v) l++;
+  return l;
+}
+bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
+
+void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block) {
+  if (!e) return;
+  e->code = code;
+  e->axis = axis;
+  e->index = index;
+  e->leaf = leaf;
+  e->block = block;
+}
+
+// Enqueue the whole block pipeline.  d_roots: nblocks * 4k records (96 B).
+int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
+                     void* d_dah, unsigned long long* d_status, hipStream_t s) {
+  const uint32_t w = 2 * k;
+  const size_t cells = (size_t)nblocks * w * w;
+  int rc = ensure(c, c->leaf, cells * CDA_REC_BYTES);
+  if (rc) return rc;
+  rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
+  if (rc) return rc;
+  const long long S = CDA_SHARE;
+  {
+    RsJob j{};
+    j.src = d_ods;
+    j.src_blk = (long long)k * k * S;
+    j.src_cw = (long long)k * S;
+    j.src_sh = S;
+    j.dst = d_eds + (size_t)k * S;
+    j.dst_blk = (long long)w * w * S;
+    j.dst_cw = (long long)w * S;
+    j.dst_sh = S;
+    j.cpy = d_eds;
+    j.cpy_blk = j.dst_blk;
+    j.cpy_cw = j.dst_cw;
+    j.cpy_sh = S;
+    j.k = (int)k;
+    j.cw_per_blk = (int)k;
+    j.nblk = (int)nblocks;
+    j.shard_len = CDA_SHARE;
+    ProfScope ps(c, "rs_encode8_rows", s);
+    if (launch_rs_encode8(j, s)) return CDA_E_DEVICE;
+  }
+  {
+    RsJob j{};
+    j.src = d_eds;
+    j.src_blk = (long long)w * w * S;
+    j.src_cw = S;
+    j.src_sh = (long long)w * S;
+    j.dst = d_eds + (size_t)k * w * S;
+    j.dst_blk = j.src_blk;
+    j.dst_cw = S;
+    j.dst_sh = (long long)w * S;
+    j.cpy = nullptr;
+    j.k = (int)k;
+    j.cw_per_blk = (int)w;
+    j.nblk = (int)nblocks;
+    j.shard_len = CDA_SHARE;
+    ProfScope ps(c, "rs_encode8_cols", s);
+    if (launch_rs_encode8(j, s)) return CDA_E_DEVICE;
+  }
+  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+  {
+    ProfScope ps(c, "leaf_hash", s);
+    if (launch_leaf_hash(d_eds, c->leaf.p, d_status, (int)k, (int)nblocks, s)) return CDA_E_DEVICE;
+  }
+  const int L = ilog2i(w);
+  void* bufs[2] = {c->leaf.p, c->scratch.p};
+  for (int level = 1; level <= L; level++) {
+    const void* in = bufs[(level - 1) & 1];
+    void* out = level == L ? d_roots : bufs[level & 1];
+    ProfScope ps(c, level == 1 ? "nmt_level1" : "nmt_level", s);
+    if (launch_nmt_level(in, out, level == 1, (int)k, (int)nblocks, level, s)) return CDA_E_DEVICE;
+  }
+  {
+    ProfScope ps(c, "dah", s);
+    if (launch_dah(d_roots, d_dah, (int)(2 * w), (int)nblocks, s)) return CDA_E_DEVICE;
+  }
+  return CDA_OK;
+}
+
+// 96-B records -> packed 90-B nodes
+void pack_roots(const uint8_t* recs, uint32_t n, uint8_t* out) {
+  for (uint32_t i = 0; i < n; i++) memcpy(out + (size_t)i * CDA_NODE_SIZE, recs + (size_t)i * CDA_REC_BYTES, CDA_NODE_SIZE);
+}
+
+int map_status(uint64_t st, int block, cda_err_info* err) {
+  if (st == ~0ull) return CDA_OK;
+  set_err(err, CDA_E_NS_ORDER, (int)(st >> 40), (int)((st >> 20) & 0xFFFFF), (int)(st & 0xFFFFF), block);
+  return CDA_E_NS_ORDER;
+}
+
+struct Lock {
+  cda_ctx* c;
+  std::lock_guard<std::recursive_mutex> g;
+  explicit Lock(cda_ctx* x) : c(x), g(x->mu) { (void)hipSetDevice(x->device); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int cda_init(int device, cda_ctx** out) {
+  if (!out) return CDA_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CDA_E_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return CDA_E_DEVICE;
+  cda_ctx* c = new cda_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || rs_init_device_tables(device)) {
+    delete c;
+    return CDA_E_DEVICE;
+  }
+  *out = c;
+  return CDA_OK;
+}
+
+void cda_free(cda_ctx* c) {
+  if (!c) return;
+  {
+    Lock l(c);
+    (void)hipStreamSynchronize(c->stream);
+    flush_profile(c);
+    for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status})
+      if (b->p) (void)hipFree(b->p);
+    if (c->host_status.p) (void)hipHostFree(c->host_status.p);
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+const char* cda_strerror(int code) {
+  switch (code) {
+    case CDA_OK: return "ok";
+    case CDA_E_NOT_POW2: return "number of shares is not a power of 2";
+    case CDA_E_NOT_SQUARE: return "number of chunks must be a square number";
+    case CDA_E_SHARD_SIZE: return "chunk size must be a multiple of 64 bytes";
+    case CDA_E_NS_SHORT: return "data is too short to contain namespace ID";
+    case CDA_E_NS_ORDER: return "pushed data has smaller namespace than previous (invalid push order)";
+    case CDA_E_TOO_FEW: return "too few shards given";
+    case CDA_E_UNREPAIRABLE: return "failed to solve data square";
+    case CDA_E_BYZANTINE: return "byzantine data";
+    case CDA_E_ARG: return "invalid argument";
+    case CDA_E_DEVICE: return "device error";
+    case CDA_E_PUSH_PAST: return "pushed past predetermined square size";
+    case CDA_E_UNSUPPORTED: return "unsupported configuration";
+    default: return "unknown error";
+  }
+}
+
+const char* cda_last_device_error(cda_ctx* c) { return c ? c->last_err.c_str() : ""; }
+
+int64_t cda_rs_max_chunks(void) { return (int64_t)32768 * 32768; }
+const char* cda_rs_name(void) { return "Leopard"; }
+int cda_rs_validate_chunk_size(int64_t chunk_size) {
+  return (chunk_size > 0 && chunk_size % 64 == 0) ? CDA_OK : CDA_E_SHARD_SIZE;
+}
+
+int cda_rs_encode(cda_ctx* c, uint32_t k, uint32_t shard_len, const uint8_t* data, uint8_t* parity) {
+  if (!c || !data || !parity || k == 0 || k > 32768) return CDA_E_ARG;
+  if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
+  Lock l(c);
+  const size_t bytes = (size_t)k * shard_len;
+  if (int rc = ensure(c, c->ods, bytes)) return rc;
+  if (int rc = ensure(c, c->eds, bytes)) return rc;
+  if (!dev_ok(c, hipMemcpyAsync(c->ods.p, data, bytes, hipMemcpyHostToDevice, c->stream), "H2D")) return CDA_E_DEVICE;
+  RsJob j{};
+  j.src = (const uint8_t*)c->ods.p;
+  j.src_sh = shard_len;
+  j.dst = (uint8_t*)c->eds.p;
+  j.dst_sh = shard_len;
+  j.k = (int)k;
+  j.cw_per_blk = 1;
+  j.nblk = 1;
+  j.shard_len = (int)shard_len;
+  int lr;
+  {
+    ProfScope ps(c, 2 * k <= 256 ? "rs_encode8" : "rs_encode16", c->stream);
+    lr = 2 * k <= 256 ? launch_rs_encode8(j, c->stream) : launch_rs_encode16(j, c->stream);
+  }
+  if (lr == -2) return CDA_E_UNSUPPORTED;
+  if (lr) return CDA_E_DEVICE;
+  if (!dev_ok(c, hipMemcpyAsync(parity, c->eds.p, bytes, hipMemcpyDeviceToHost, c->stream), "D2H")) return CDA_E_DEVICE;
+  if (!dev_ok(c, hipStreamSynchronize(c->stream), "sync")) return CDA_E_DEVICE;
+  flush_profile(c);
+  return CDA_OK;
+}
+
+int cda_rs_decode(cda_ctx* c, uint32_t k, uint32_t shard_len, uint8_t* shards, const uint8_t* present) {
+  if (!c || !shards || !present || k == 0 || k > 32768) return CDA_E_ARG;
+  if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
+  uint32_t np = 0;
+  for (uint32_t i = 0; i < 2 * k; i++) np += present[i] ? 1 : 0;
+  if (np < k) return CDA_E_TOO_FEW;
+  if (np == 2 * k) return CDA_OK;
+  return CDA_E_UNSUPPORTED;
+}
+
+int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds, void* d_roots,
+                             void* d_dah, void* d_status, void* stream) {
+  if (!c || !d_ods || !d_eds || !d_roots || !d_dah || !d_status || nblocks == 0) return CDA_E_ARG;
+  if (!is_pow2(k) || k > 128) return k > 128 ? CDA_E_UNSUPPORTED : CDA_E_NOT_POW2;
+  Lock l(c);
+  hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  return enqueue_pipeline(c, k, nblocks, (const uint8_t*)d_ods, (uint8_t*)d_eds, d_roots, d_dah,
+                          (unsigned long long*)d_status, s);
+}
+
+int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
+                            uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !ods || !row_roots || !col_roots || !dah || nblocks == 0) return CDA_E_ARG;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  if (k > 128) return CDA_E_UNSUPPORTED;
+  Lock l(c);
+  const uint32_t w = 2 * k;
+  const size_t ods_b = (size_t)nblocks * k * k * CDA_SHARE, eds_b = (size_t)nblocks * w * w * CDA_SHARE;
+  const size_t roots_b = (size_t)nblocks * 2 * w * CDA_REC_BYTES;
+  int rc;
+  if ((rc = ensure(c, c->ods, ods_b)) || (rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->roots, roots_b)) ||
+      (rc = ensure(c, c->dah, (size_t)nblocks * 32)) || (rc = ensure(c, c->status, (size_t)nblocks * 8)))
+    return rc;
+  if (!dev_ok(c, hipMemcpyAsync(c->ods.p, ods, ods_b, hipMemcpyHostToDevice, c->stream), "H2D")) return CDA_E_DEVICE;
+  rc = enqueue_pipeline(c, k, nblocks, (const uint8_t*)c->ods.p, (uint8_t*)c->eds.p, c->roots.p, c->dah.p,
+                        (unsigned long long*)c->status.p, c->stream);
+  if (rc) return rc;
+  std::vector<uint8_t> recs(roots_b);
+  std::vector<uint64_t> st(nblocks);
+  if (eds_or_null &&
+      !dev_ok(c, hipMemcpyAsync(eds_or_null, c->eds.p, eds_b, hipMemcpyDeviceToHost, c->stream), "D2H"))
+    return CDA_E_DEVICE;
+  if (!dev_ok(c, hipMemcpyAsync(recs.data(), c->roots.p, roots_b, hipMemcpyDeviceToHost, c->stream), "D2H") ||
+      !dev_ok(c, hipMemcpyAsync(dah, c->dah.p, (size_t)nblocks * 32, hipMemcpyDeviceToHost, c->stream), "D2H") ||
+      !dev_ok(c, hipMemcpyAsync(st.data(), c->status.p, (size_t)nblocks * 8, hipMemcpyDeviceToHost, c->stream), "D2H") ||
+      !dev_ok(c, hipStreamSynchronize(c->stream), "sync"))
+    return CDA_E_DEVICE;
+  flush_profile(c);
+  for (uint32_t b = 0; b < nblocks; b++) {
+    const uint8_t* r = recs.data() + (size_t)b * 2 * w * CDA_REC_BYTES;
+    pack_roots(r, w, row_roots + (size_t)b * w * CDA_NODE_SIZE);
+    pack_roots(r + (size_t)w * CDA_REC_BYTES, w, col_roots + (size_t)b * w * CDA_NODE_SIZE);
+  }
+  for (uint32_t b = 0; b < nblocks; b++)
+    if ((rc = map_status(st[b], (int)b, err))) return rc;
+  return CDA_OK;
+}
+
+int cda_extend_commit(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares, uint8_t* eds_or_null,
+                      uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !shares || !row_roots || !col_roots || !dah) return CDA_E_ARG;
+  // da.ExtendShares: power-of-two check (data_availability_header.go:67-69)
+  if (!is_pow2(count)) return set_err(err, CDA_E_NOT_POW2, -1, -1, -1, -1), CDA_E_NOT_POW2;
+  // rsmt2d ComputeExtendedDataSquare: square count, chunk size
+  const uint32_t k = (uint32_t)std::ceil(std::sqrt((double)count));
+  if (k * k != count) return set_err(err, CDA_E_NOT_SQUARE, -1, -1, -1, -1), CDA_E_NOT_SQUARE;
+  if (cda_rs_validate_chunk_size(share_len)) return CDA_E_SHARD_SIZE;
+  if (share_len != CDA_SHARE) return CDA_E_UNSUPPORTED;
+  return cda_extend_commit_batch(c, k, 1, shares, eds_or_null, row_roots, col_roots, dah, err);
+}
+
+int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                   cda_err_info* err) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !eds || !row_roots || !col_roots || !dah) return CDA_E_ARG;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  Lock l(c);
+  const uint32_t w = 2 * k;
+  const size_t eds_b = (size_t)w * w * CDA_SHARE, roots_b = (size_t)2 * w * CDA_REC_BYTES;
+  int rc;
+  if ((rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->roots, roots_b)) || (rc = ensure(c, c->dah, 32)) ||
+      (rc = ensure(c, c->status, 8)) || (rc = ensure(c, c->leaf, (size_t)w * w * CDA_REC_BYTES)) ||
+      (rc = ensure(c, c->scratch, (size_t)w * w * CDA_REC_BYTES)))
+    return rc;
+  hipStream_t s = c->stream;
+  if (!dev_ok(c, hipMemcpyAsync(c->eds.p, eds, eds_b, hipMemcpyHostToDevice, s), "H2D") ||
+      !dev_ok(c, hipMemsetAsync(c->status.p, 0xFF, 8, s), "memset"))
+    return CDA_E_DEVICE;
+  {
+    ProfScope ps(c, "leaf_hash", s);
+    if (launch_leaf_hash((const uint8_t*)c->eds.p, c->leaf.p, (unsigned long long*)c->status.p, (int)k, 1, s))
+      return CDA_E_DEVICE;
+  }
+  const int L = ilog2i(w);
+  void* bufs[2] = {c->leaf.p, c->scratch.p};
+  for (int level = 1; level <= L; level++) {
+    ProfScope ps(c, "nmt_level", s);
+    if (launch_nmt_level(bufs[(level - 1) & 1], level == L ? c->roots.p : bufs[level & 1], level == 1, (int)k, 1,
+                         level, s))
+      return CDA_E_DEVICE;
+  }
+  {
+    ProfScope ps(c, "dah", s);
+    if (launch_dah(c->roots.p, c->dah.p, (int)(2 * w), 1, s)) return CDA_E_DEVICE;
+  }
+  std::vector<uint8_t> recs(roots_b);
+  uint64_t st = 0;
+  if (!dev_ok(c, hipMemcpyAsync(recs.data(), c->roots.p, roots_b, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipMemcpyAsync(dah, c->dah.p, 32, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipMemcpyAsync(&st, c->status.p, 8, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipStreamSynchronize(s), "sync"))
+    return CDA_E_DEVICE;
+  flush_profile(c);
+  pack_roots(recs.data(), w, row_roots);
+  pack_roots(recs.data() + (size_t)w * CDA_REC_BYTES, w, col_roots);
+  return map_status(st, 0, err);
+}
+
+int cda_dah_hash(cda_ctx* c, uint32_t n, const uint8_t* row_roots, const uint8_t* col_roots, uint8_t* dah) {
+  if (!c || !dah) return CDA_E_ARG;
+  if (n == 0) {  // merkle.HashFromByteSlices(nil) = SHA256("")
+    static const uint8_t kEmpty[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                                       0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                                       0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+    memcpy(dah, kEmpty, 32);
+    return CDA_OK;
+  }
+  if (!row_roots || !col_roots) return CDA_E_ARG;
+  Lock l(c);
+  const size_t roots_b = (size_t)2 * n * CDA_REC_BYTES;
+  int rc;
+  if ((rc = ensure(c, c->roots, roots_b)) || (rc = ensure(c, c->dah, 32))) return rc;
+  std::vector<uint8_t> recs(roots_b, 0);
+  for (uint32_t i = 0; i < n; i++) {
+    memcpy(recs.data() + (size_t)i * CDA_REC_BYTES, row_roots + (size_t)i * CDA_NODE_SIZE, CDA_NODE_SIZE);
+    memcpy(recs.data() + (size_t)(n + i) * CDA_REC_BYTES, col_roots + (size_t)i * CDA_NODE_SIZE, CDA_NODE_SIZE);
+  }
+  hipStream_t s = c->stream;
+  if (!dev_ok(c, hipMemcpyAsync(c->roots.p, recs.data(), roots_b, hipMemcpyHostToDevice, s), "H2D"))
+    return CDA_E_DEVICE;
+  {
+    ProfScope ps(c, "dah", s);
+    int lr = launch_dah(c->roots.p, c->dah.p, (int)(2 * n), 1, s);
+    if (lr == -2) return CDA_E_UNSUPPORTED;
+    if (lr) return CDA_E_DEVICE;
+  }
+  if (!dev_ok(c, hipMemcpyAsync(dah, c->dah.p, 32, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipStreamSynchronize(s), "sync"))
+    return CDA_E_DEVICE;
+  flush_profile(c);
+  return CDA_OK;
+}
+
+int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uint32_t n, uint32_t leaf_len,
+                      const uint8_t* leaves, uint8_t* root, cda_err_info* err) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !root || (n && !leaves) || square_size == 0) return CDA_E_ARG;
+  // ErasuredNamespacedMerkleTree.Push checks, in the reference's order (nmt_wrapper.go:94-99)
+  for (uint32_t i = 0; i < n; i++) {
+    if (axis_index + 1 > 2 * square_size || (uint64_t)i + 1 > 2 * square_size)
+      return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, (int)i, -1), CDA_E_PUSH_PAST;
+    if (leaf_len < CDA_NAMESPACE_SIZE) return set_err(err, CDA_E_NS_SHORT, -1, (int)axis_index, (int)i, -1), CDA_E_NS_SHORT;
+  }
+  if (n == 0) {  // EmptyRoot: 0x00*58 ‖ SHA256("")
+    static const uint8_t kEmpty[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                                       0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                                       0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+    memset(root, 0, 58);
+    memcpy(root + 58, kEmpty, 32);
+    return CDA_OK;
+  }
+  if (leaf_len != CDA_SHARE) return CDA_E_UNSUPPORTED;
+  Lock l(c);
+  const size_t in_b = (size_t)n * leaf_len, rec_b = (size_t)n * CDA_REC_BYTES;
+  int rc;
+  if ((rc = ensure(c, c->ods, in_b)) || (rc = ensure(c, c->leaf, rec_b)) || (rc = ensure(c, c->scratch, rec_b)) ||
+      (rc = ensure(c, c->status, 8)))
+    return rc;
+  hipStream_t s = c->stream;
+  if (!dev_ok(c, hipMemcpyAsync(c->ods.p, leaves, in_b, hipMemcpyHostToDevice, s), "H2D") ||
+      !dev_ok(c, hipMemsetAsync(c->status.p, 0xFF, 8, s), "memset"))
+    return CDA_E_DEVICE;
+  {
+    ProfScope ps(c, "axis_leaf", s);
+    if (launch_axis_leaf((const uint8_t*)c->ods.p, (int)n, square_size, axis_index, c->leaf.p,
+                         (unsigned long long*)c->status.p, s))
+      return CDA_E_DEVICE;
+  }
+  void* bufs[2] = {c->leaf.p, c->scratch.p};
+  int cur = 0;
+  for (uint32_t cnt = n; cnt > 1; cnt = (cnt + 1) / 2) {
+    ProfScope ps(c, "nmt_level_generic", s);
+    if (launch_level_generic(bufs[cur], bufs[cur ^ 1], (int)cnt, s)) return CDA_E_DEVICE;
+    cur ^= 1;
+  }
+  uint8_t rec[CDA_REC_BYTES];
+  uint64_t st = 0;
+  if (!dev_ok(c, hipMemcpyAsync(rec, bufs[cur], CDA_REC_BYTES, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipMemcpyAsync(&st, c->status.p, 8, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipStreamSynchronize(s), "sync"))
+    return CDA_E_DEVICE;
+  flush_profile(c);
+  if (st != ~0ull) return set_err(err, CDA_E_NS_ORDER, -1, (int)axis_index, (int)st, -1), CDA_E_NS_ORDER;
+  memcpy(root, rec, CDA_NODE_SIZE);
+  return CDA_OK;
+}
+
+int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+               const uint8_t* col_roots, cda_err_info* err) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
+  return CDA_E_UNSUPPORTED;
+}
+
+int cda_profile_enable(cda_ctx* c, int enable) {
+  if (!c) return CDA_E_ARG;
+  Lock l(c);
+  c->prof = enable != 0;
+  return CDA_OK;
+}
+
+int cda_profile_reset(cda_ctx* c) {
+  if (!c) return CDA_E_ARG;
+  Lock l(c);
+  flush_profile(c);
+  c->prof_acc.clear();
+  return CDA_OK;
+}
+
+int cda_profile_read(cda_ctx* c, char* names_buf, size_t names_cap, double* total_ms, int64_t* launches, int cap) {
+  if (!c) return CDA_E_ARG;
+  Lock l(c);
+  flush_profile(c);
+  int i = 0;
+  size_t off = 0;
+  for (auto& kv : c->prof_acc) {
+    if (i >= cap) break;
+    const size_t len = kv.first.size() + 1;
+    if (names_buf && off + len <= names_cap) {
+      memcpy(names_buf + off, kv.first.c_str(), len);
+      off += len;
+    }
+    if (total_ms) total_ms[i] = kv.second.first;
+    if (launches) launches[i] = kv.second.second;
+    i++;
+  }
+  return i;
+}
+
+}  // extern "C"

@@ -1,0 +1,450 @@
+// nmt_kernels.hip — erasured-NMT leaf/inner hashing and the DAH RFC-6962 tree.
+//
+// Reference semantics (celestia-app @ 2025-02-13):
+//   leaf:  ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share), ns = share[0:29] in Q0 else 0xFF×29
+//          pkg/wrapper/nmt_wrapper.go:93-114,138-140; test/util/malicious/hasher.go:186-209
+//   node:  L.min ‖ (R.min == 0xFF×29 ? L.max : R.max) ‖ SHA256(0x01 ‖ L ‖ R)
+//          hasher.go:271-310 (IgnoreMaxNamespace=true, nmt_wrapper.go:60)
+//   DAH:   RFC-6962 over row roots ‖ col roots, pkg/da/data_availability_header.go:92-108
+//
+// Design (MI355X): the leaf data of cell (r,c) is identical in row tree r and
+// column tree c (both use the share's namespace iff the cell is in Q0), so each
+// of the 4k² cells is hashed ONCE (the reference hashes it twice) and both trees
+// read the same 96-byte leaf record.  Records are 96 B (90-B node + 6 zero bytes)
+// so a node is six 16-B loads/stores.  Inner levels are one launch per level over
+// every tree of every block in the batch (4k trees/block, lanes stay full until
+// the last few levels).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cda_internal.h"
+#include "sha256_dev.h"
+
+namespace cda {
+
+// ---------------------------------------------------------------------------
+// Leaf hashing: one thread per EDS cell.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load16(const uint4* p, uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint4 v = p[i];
+    w[4 * i + 0] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+
+// Big-endian namespace words of a 29-byte namespace held little-endian in n[0..7]
+// (n[7] byte 0 = ns[28]) compared lexicographically: returns -1/0/1.
+__device__ __forceinline__ int ns_cmp(const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t x = bswap(a[i]), y = bswap(b[i]);
+    if (i == 7) {
+      x >>= 24;
+      y >>= 24;
+    }
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return 0;
+}
+
+// Leaf record of one 512-B share whose first 64 bytes are already in A[0..16):
+// ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share) ‖ 6 zero bytes, ns = share[0:29] if q0 else 0xFF×29.
+__device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q0, uint4* out) {
+  uint32_t ns[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ns[i] = q0 ? A[i] : 0xFFFFFFFFu;
+  uint32_t st[8];
+  sha256_init(st);
+  uint32_t m[16];
+  // block 0: 0x00 ‖ ns[0..29) ‖ share[0..34)
+  if (q0) {
+    m[0] = be_window(0u, A[0], 3);
+#pragma unroll
+    for (int i = 1; i < 7; i++) m[i] = be_window(A[i - 1], A[i], 3);
+    // bytes 28..31 = ns[27], ns[28], share[0], share[1]
+    m[7] = (be_window(A[6], A[7], 3) & 0xFFFF0000u) | (bswap(A[0]) >> 16);
+  } else {
+    m[0] = 0x00FFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 7; i++) m[i] = 0xFFFFFFFFu;
+    m[7] = 0xFFFF0000u | (bswap(A[0]) >> 16);
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) m[i] = be_window(A[i - 8], A[i - 7], 2);
+  sha256_compress(st, m);
+  // blocks 1..7: message words 16j..16j+15 = share bytes 64j-30.. : windows of S[16j-8 .. 16j+8].
+  // H carries the upper half of the previous 16-word chunk.
+  uint32_t H[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) H[i] = A[8 + i];
+#pragma unroll
+  for (int j = 1; j < 8; j++) {
+    uint32_t C[16];
+    load16(sh + 4 * j, C);
+#pragma unroll
+    for (int i = 0; i < 7; i++) m[i] = be_window(H[i], H[i + 1], 2);
+    m[7] = be_window(H[7], C[0], 2);
+#pragma unroll
+    for (int i = 8; i < 16; i++) m[i] = be_window(C[i - 8], C[i - 7], 2);
+    sha256_compress(st, m);
+#pragma unroll
+    for (int i = 0; i < 8; i++) H[i] = C[8 + i];
+  }
+  // block 8: share bytes 482..511, 0x80, zeros, bit length 542*8
+#pragma unroll
+  for (int i = 0; i < 7; i++) m[i] = be_window(H[i], H[i + 1], 2);
+  m[7] = be_window(H[7], 0x80u, 2);
+#pragma unroll
+  for (int i = 8; i < 15; i++) m[i] = 0;
+  m[15] = 542u * 8u;
+  sha256_compress(st, m);
+  // record: ns ‖ ns ‖ digest ‖ 6 zero bytes
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = bswap(st[i]);
+  uint32_t o[24];
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = ns[i];
+  o[7] = (ns[7] & 0xFFu) | (ns[0] << 8);
+#pragma unroll
+  for (int i = 8; i < 14; i++) o[i] = le_window(ns[i - 8], ns[i - 7], 3);
+  o[14] = (le_window(ns[6], ns[7], 3) & 0xFFFFu) | (d[0] << 16);
+#pragma unroll
+  for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
+  o[22] = d[7] >> 16;
+  o[23] = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) out[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
+
+__global__ void __launch_bounds__(256) leaf_hash_kernel(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
+                                                        unsigned long long* __restrict__ status, int k, int log2w,
+                                                        uint32_t total_cells) {
+  uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total_cells) return;
+  const int w = 1 << log2w;
+  const uint32_t cell = gid & ((1u << (2 * log2w)) - 1);
+  const uint32_t blk = gid >> (2 * log2w);
+  const int r = (int)(cell >> log2w), c = (int)(cell & (w - 1));
+  const bool q0 = (r < k) && (c < k);
+  const uint4* sh = reinterpret_cast<const uint4*>(eds + (size_t)gid * CDA_SHARE);
+
+  uint32_t A[16];
+  load16(sh, A);
+  uint32_t ns[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ns[i] = A[i];
+
+  // Namespace order (nmt Push ErrInvalidPushOrder) — checked for Q0 neighbours;
+  // parity leaves carry 0xFF×29, the maximum, so only Q0 pairs can violate it.
+  if (q0) {
+    if (c + 1 < k) {
+      uint32_t nb[8];
+      const uint4* p = reinterpret_cast<const uint4*>(eds + ((size_t)gid + 1) * CDA_SHARE);
+      uint4 v0 = p[0], v1 = p[1];
+      nb[0] = v0.x; nb[1] = v0.y; nb[2] = v0.z; nb[3] = v0.w;
+      nb[4] = v1.x; nb[5] = v1.y; nb[6] = v1.z; nb[7] = v1.w;
+      if (ns_cmp(nb, ns) < 0) {
+        unsigned long long key = ((unsigned long long)CDA_AXIS_ROW << 40) | ((unsigned long long)r << 20) | (c + 1);
+        atomicMin(status + blk, key);
+      }
+    }
+    if (r + 1 < k) {
+      uint32_t nb[8];
+      const uint4* p = reinterpret_cast<const uint4*>(eds + ((size_t)gid + w) * CDA_SHARE);
+      uint4 v0 = p[0], v1 = p[1];
+      nb[0] = v0.x; nb[1] = v0.y; nb[2] = v0.z; nb[3] = v0.w;
+      nb[4] = v1.x; nb[5] = v1.y; nb[6] = v1.z; nb[7] = v1.w;
+      if (ns_cmp(nb, ns) < 0) {
+        unsigned long long key = ((unsigned long long)CDA_AXIS_COL << 40) | ((unsigned long long)c << 20) | (r + 1);
+        atomicMin(status + blk, key);
+      }
+    }
+  }
+
+  leaf_record(sh, A, q0, nodes + (size_t)gid * 6);
+}
+
+// ---------------------------------------------------------------------------
+// Inner NMT node.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_node(const uint4* p, uint32_t* n) {
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    uint4 v = p[i];
+    n[4 * i + 0] = v.x;
+    n[4 * i + 1] = v.y;
+    n[4 * i + 2] = v.z;
+    n[4 * i + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void hash_node(const uint32_t* L, const uint32_t* R, uint32_t* o) {
+  uint32_t st[8];
+  sha256_init(st);
+  uint32_t m[16];
+  // message = 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits); 48 words
+  // block 0: words 0..15
+  m[0] = be_window(0x01000000u, L[0], 3);
+#pragma unroll
+  for (int i = 1; i < 16; i++) m[i] = be_window(L[i - 1], L[i], 3);
+  sha256_compress(st, m);
+  // block 1: words 16..31
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int wi = 16 + i;
+    if (wi <= 21) m[i] = be_window(L[wi - 1], L[wi], 3);
+    else if (wi == 22) m[i] = be_window(L[21], L[22], 3) | (R[0] & 0xFFu);
+    else m[i] = be_window(R[wi - 23], R[wi - 22], 1);
+  }
+  sha256_compress(st, m);
+  // block 2: words 32..47
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int wi = 32 + i;
+    if (wi <= 44) m[i] = be_window(R[wi - 23], R[wi - 22], 1);
+    else if (wi == 45) m[i] = be_window(R[22], R[23], 1) | 0x00800000u;
+    else if (wi == 46) m[i] = 0;
+    else m[i] = 181u * 8u;
+  }
+  sha256_compress(st, m);
+
+  // namespace range: min = L.min; max = R.min == parity ns ? L.max : R.max
+  bool rmin_max = true;
+#pragma unroll
+  for (int i = 0; i < 7; i++) rmin_max &= (R[i] == 0xFFFFFFFFu);
+  rmin_max &= ((R[7] & 0xFFu) == 0xFFu);
+  uint32_t S[24];
+#pragma unroll
+  for (int i = 7; i < 15; i++) S[i] = rmin_max ? L[i] : R[i];
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = bswap(st[i]);
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = L[i];
+  o[7] = (L[7] & 0xFFu) | (S[7] & 0xFFFFFF00u);
+#pragma unroll
+  for (int i = 8; i < 14; i++) o[i] = S[i];
+  o[14] = (S[14] & 0xFFFFu) | (d[0] << 16);
+#pragma unroll
+  for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
+  o[22] = d[7] >> 16;
+  o[23] = 0;
+}
+
+// One thread per output node. Level 1 reads leaf records in cell-major layout
+// ([blk][r][c]); later levels read [blk][tree][n_in].  Trees 0..w-1 are rows,
+// w..2w-1 columns.
+template <bool FROM_LEAVES>
+__global__ void __launch_bounds__(256) nmt_level_kernel(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                        int log2w, int log2n_out, uint32_t total_out) {
+  uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total_out) return;
+  const int w = 1 << log2w;
+  const uint32_t j = gid & ((1u << log2n_out) - 1);
+  const uint32_t tree_g = gid >> log2n_out;  // blk * 2w + tree
+  const uint32_t blk = tree_g >> (log2w + 1);
+  const uint32_t tree = tree_g & (2 * w - 1);
+  size_t ia, ib;
+  if (FROM_LEAVES) {
+    const size_t base = (size_t)blk << (2 * log2w);
+    if (tree < (uint32_t)w) {  // row tree: cells (tree, 2j), (tree, 2j+1)
+      ia = base + ((size_t)tree << log2w) + 2 * j;
+      ib = ia + 1;
+    } else {  // column tree: cells (2j, col), (2j+1, col)
+      const uint32_t col = tree - w;
+      ia = base + ((size_t)(2 * j) << log2w) + col;
+      ib = ia + w;
+    }
+  } else {
+    ia = ((size_t)tree_g << (log2n_out + 1)) + 2 * j;
+    ib = ia + 1;
+  }
+  uint32_t L[24], R[24], o[24];
+  load_node(in + ia * 6, L);
+  load_node(in + ib * 6, R);
+  hash_node(L, R, o);
+  uint4* po = out + (size_t)gid * 6;
+#pragma unroll
+  for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
+
+// ---------------------------------------------------------------------------
+// DAH: RFC-6962 over the n = 2w roots (rows then cols), one workgroup per block.
+// Levels pair (2i, 2i+1) and promote an odd last node, which is the same tree as
+// HashFromByteSlices' "split at the largest power of two below n" recursion.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ roots, uint32_t* __restrict__ dah,
+                                                  int n) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sdig[];  // [n + (n+1)/2][8] big-endian digests
+  const uint32_t blk = blockIdx.x;
+  const uint4* rb = roots + (size_t)blk * n * 6;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t L[24];
+    load_node(rb + (size_t)i * 6, L);
+    uint32_t st[8], m[16];
+    sha256_init(st);
+    // 0x00 ‖ root[0..90) ‖ 0x80 ‖ ... ‖ len(91*8)
+    m[0] = be_window(0u, L[0], 3);
+#pragma unroll
+    for (int t = 1; t < 16; t++) m[t] = be_window(L[t - 1], L[t], 3);
+    sha256_compress(st, m);
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      const int wi = 16 + t;
+      if (wi <= 21) m[t] = be_window(L[wi - 1], L[wi], 3);
+      else if (wi == 22) m[t] = be_window(L[21], L[22], 3) | 0x80u;
+      else if (wi < 31) m[t] = 0;
+      else m[t] = 91u * 8u;
+    }
+    sha256_compress(st, m);
+#pragma unroll
+    for (int t = 0; t < 8; t++) sdig[i * 8 + t] = st[t];
+  }
+  __syncthreads();
+  uint32_t* src = sdig;
+  uint32_t* dst = sdig + n * 8;
+  for (int cnt = n; cnt > 1;) {
+    const int out_cnt = (cnt + 1) >> 1;
+    for (int i = threadIdx.x; i < out_cnt; i += blockDim.x) {
+      uint32_t* o = dst + i * 8;
+      const uint32_t* Ld = src + (2 * i) * 8;
+      if (2 * i + 1 >= cnt) {
+#pragma unroll
+        for (int t = 0; t < 8; t++) o[t] = Ld[t];
+        continue;
+      }
+      const uint32_t* Rd = src + (2 * i + 1) * 8;
+      uint32_t st[8], m[16];
+      sha256_init(st);
+      m[0] = 0x01000000u | (Ld[0] >> 8);
+#pragma unroll
+      for (int t = 1; t < 8; t++) m[t] = (Ld[t - 1] << 24) | (Ld[t] >> 8);
+      m[8] = (Ld[7] << 24) | (Rd[0] >> 8);
+#pragma unroll
+      for (int t = 9; t < 16; t++) m[t] = (Rd[t - 9] << 24) | (Rd[t - 8] >> 8);
+      sha256_compress(st, m);
+      m[0] = (Rd[7] << 24) | 0x00800000u;
+#pragma unroll
+      for (int t = 1; t < 15; t++) m[t] = 0;
+      m[15] = 65u * 8u;
+      sha256_compress(st, m);
+#pragma unroll
+      for (int t = 0; t < 8; t++) o[t] = st[t];
+    }
+    __syncthreads();
+    uint32_t* tmp = src;
+    src = dst;
+    dst = tmp;
+    cnt = out_cnt;
+  }
+  if (threadIdx.x < 8) dah[blk * 8 + threadIdx.x] = bswap(src[threadIdx.x]);
+}
+
+// ---------------------------------------------------------------------------
+// Single-axis tree (wrapper.NewConstructor(k)(axis, index) with n Pushes).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) axis_leaf_kernel(const uint8_t* __restrict__ leaves, int n,
+                                                        unsigned long long square_size,
+                                                        unsigned long long axis_index, uint4* __restrict__ nodes,
+                                                        unsigned long long* __restrict__ status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool q0 = ((unsigned long long)i < square_size) && (axis_index < square_size);
+  const uint4* sh = reinterpret_cast<const uint4*>(leaves + (size_t)i * CDA_SHARE);
+  uint32_t A[16];
+  load16(sh, A);
+  // Push order: leaf i+1 (if also in Q0) must not have a smaller namespace
+  if (q0 && (unsigned long long)(i + 1) < square_size && i + 1 < n) {
+    uint32_t nb[8];
+    const uint4* p = sh + CDA_SHARE / 16;
+    uint4 v0 = p[0], v1 = p[1];
+    nb[0] = v0.x; nb[1] = v0.y; nb[2] = v0.z; nb[3] = v0.w;
+    nb[4] = v1.x; nb[5] = v1.y; nb[6] = v1.z; nb[7] = v1.w;
+    if (ns_cmp(nb, A) < 0) atomicMin(status, (unsigned long long)(i + 1));
+  }
+  leaf_record(sh, A, q0, nodes + (size_t)i * 6);
+}
+
+__global__ void __launch_bounds__(256) level_generic_kernel(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                            int n_in) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_out = (n_in + 1) >> 1;
+  if (j >= n_out) return;
+  uint4* po = out + (size_t)j * 6;
+  if (2 * j + 1 >= n_in) {  // odd node is promoted unchanged
+#pragma unroll
+    for (int i = 0; i < 6; i++) po[i] = in[(size_t)(2 * j) * 6 + i];
+    return;
+  }
+  uint32_t L[24], R[24], o[24];
+  load_node(in + (size_t)(2 * j) * 6, L);
+  load_node(in + (size_t)(2 * j + 1) * 6, R);
+  hash_node(L, R, o);
+#pragma unroll
+  for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
+                     hipStream_t s) {
+  const int w = 2 * k;
+  int log2w = 0;
+  while ((1 << log2w) < w) log2w++;
+  const uint32_t total = (uint32_t)nblocks * (uint32_t)w * (uint32_t)w;
+  const uint32_t grid = (total + 255) / 256;
+  hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k, log2w,
+                     total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int nblocks, int level,
+                     hipStream_t s) {
+  const int w = 2 * k;
+  int log2w = 0;
+  while ((1 << log2w) < w) log2w++;
+  const int log2n_out = log2w - level;
+  const uint32_t total = (uint32_t)nblocks * (uint32_t)(2 * w) * (1u << log2n_out);
+  const uint32_t grid = (total + 255) / 256;
+  if (from_leaves)
+    hipLaunchKernelGGL(nmt_level_kernel<true>, dim3(grid), dim3(256), 0, s, (const uint4*)d_in, (uint4*)d_out, log2w,
+                       log2n_out, total);
+  else
+    hipLaunchKernelGGL(nmt_level_kernel<false>, dim3(grid), dim3(256), 0, s, (const uint4*)d_in, (uint4*)d_out,
+                       log2w, log2n_out, total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s) {
+  if (n_roots_total < 1) return -2;
+  const size_t lds = ((size_t)n_roots_total + (n_roots_total + 1) / 2) * 32;
+  if (lds > 160 * 1024) return -2;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)dah_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(dah_kernel, dim3(nblocks), dim3(256), lds, s, (const uint4*)d_roots, (uint32_t*)d_dah,
+                     n_roots_total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,
+                     unsigned long long* d_status, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(axis_leaf_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_leaves, n,
+                     (unsigned long long)square_size, (unsigned long long)axis_index, (uint4*)d_nodes, d_status);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_level_generic(const void* d_in, void* d_out, int n_in, hipStream_t s) {
+  const int n_out = (n_in + 1) / 2;
+  hipLaunchKernelGGL(level_generic_kernel, dim3((n_out + 255) / 256), dim3(256), 0, s, (const uint4*)d_in,
+                     (uint4*)d_out, n_in);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cda

@@ -1,0 +1,100 @@
+// sha256_dev.h — SHA-256 compression for gfx950 (CDNA4).
+//
+// The DA path spends ~75% of its instructions here.  gfx950
+// has a 3-input arbitrary bitwise op (v_bitop3_b32) and a funnel shift
+// (v_alignbit_b32), so one round is 14 VALU ops:
+//   Σ1 = 3 alignbit + 1 bitop3(0x96), Ch = bitop3(0xCA), Σ0 = 4, Maj = bitop3(0xE8),
+//   T1/T2/e/a = 2 add3 + 2 add.
+// Message-schedule word: σ0/σ1 = 2 alignbit + shift + bitop3 each, 2 adds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cda {
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// Big-endian word made of bytes [off, off+4) of the little-endian 8-byte
+// concatenation lo ‖ hi (lo holds bytes 0..3).  v_alignbyte_b32 computes
+// ({hi,lo} >> 8*off)[31:0]; using the builtin (not a 64-bit shift) keeps
+// InstCombine from turning neighbouring windows into unaligned scratch loads.
+__device__ __forceinline__ uint32_t le_window(uint32_t lo, uint32_t hi, int off) {
+  return off == 0 ? lo : __builtin_amdgcn_alignbyte(hi, lo, off);
+}
+__device__ __forceinline__ uint32_t be_window(uint32_t lo, uint32_t hi, int off) {
+  return bswap(le_window(lo, hi, off));
+}
+
+// Round constants; the unrolled rounds index this constexpr table so each K
+// folds into an s_mov literal.
+struct K256 {
+  static constexpr uint32_t v[64] = {
+      0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+      0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+      0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+      0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+      0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+      0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+      0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+      0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+};
+
+__device__ __forceinline__ void sha256_init(uint32_t s[8]) {
+  s[0] = 0x6a09e667;
+  s[1] = 0xbb67ae85;
+  s[2] = 0x3c6ef372;
+  s[3] = 0xa54ff53a;
+  s[4] = 0x510e527f;
+  s[5] = 0x9b05688c;
+  s[6] = 0x1f83d9ab;
+  s[7] = 0x5be0cd19;
+}
+
+// One compression of a 16-word big-endian block (w is clobbered: used as the
+// rolling message schedule).
+__device__ __forceinline__ void sha256_compress(uint32_t s[8], uint32_t w[16]) {
+  uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+  for (int t = 0; t < 64; t++) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + K256::v[t] + wt;
+    uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  s[0] += a;
+  s[1] += b;
+  s[2] += c;
+  s[3] += d;
+  s[4] += e;
+  s[5] += f;
+  s[6] += g;
+  s[7] += h;
+}
+
+}  // namespace cda

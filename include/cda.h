@@ -1,0 +1,146 @@
+/*
+ * cda.h — C ABI of the MI355X data-availability engine (libcda.so).
+ *
+ * Drop-in boundary for celestia-app's DA hot path.  Every entry
+ * point takes plain pointers and sizes, returns 0 on success or a negative
+ * CDA_E_* code, never aborts, and never retains a caller pointer after it
+ * returns (cgo rule).  Each function cites the reference interface it replaces
+ * (paths relative to the celestia-app reference tree).
+ *
+ * Threading: a cda_ctx serialises its own calls with an internal mutex, so the
+ * entry points are re-entrant from concurrent goroutines (rsmt2d calls
+ * Codec.Encode / Decode / NewTree concurrently per axis); use one ctx per OS
+ * thread for parallel submission.
+ */
+#ifndef CDA_H
+#define CDA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CDA_SHARE_SIZE 512    /* appconsts.ShareSize, pkg/appconsts/global_consts.go:29 */
+#define CDA_NAMESPACE_SIZE 29 /* appconsts.NamespaceSize, global_consts.go:26 */
+#define CDA_NODE_SIZE 90      /* NMT node = min ns ‖ max ns ‖ sha256 (test/util/malicious/app_test.go:58) */
+#define CDA_HASH_SIZE 32
+
+enum {
+  CDA_OK = 0,
+  CDA_E_NOT_POW2 = -1,     /* da.ExtendShares "number of shares is not a power of 2" (data_availability_header.go:67-69) */
+  CDA_E_NOT_SQUARE = -2,   /* rsmt2d newDataSquare "number of chunks must be a square number" */
+  CDA_E_SHARD_SIZE = -3,   /* LeoRSCodec.ValidateChunkSize: chunk size % 64 != 0 / uneven chunks */
+  CDA_E_NS_SHORT = -4,     /* wrapper Push "data is too short to contain namespace ID" (nmt_wrapper.go:97-99) */
+  CDA_E_NS_ORDER = -5,     /* nmt ErrInvalidPushOrder (leaf namespaces must be non-decreasing) */
+  CDA_E_TOO_FEW = -6,      /* reedsolomon ErrTooFewShards (Decode with < k shards) */
+  CDA_E_UNREPAIRABLE = -7, /* rsmt2d ErrUnrepairableDataSquare */
+  CDA_E_BYZANTINE = -8,    /* rsmt2d ErrByzantineData{Axis, Index} */
+  CDA_E_ARG = -9,          /* invalid argument (null pointer, k out of range, ...) */
+  CDA_E_DEVICE = -10,      /* HIP runtime / device failure */
+  CDA_E_PUSH_PAST = -11,   /* wrapper Push "pushed past predetermined square size" (nmt_wrapper.go:94-96) */
+  CDA_E_UNSUPPORTED = -12, /* configuration not implemented on the device path */
+};
+
+enum { CDA_AXIS_ROW = 0, CDA_AXIS_COL = 1 }; /* rsmt2d.Row / rsmt2d.Col */
+
+typedef struct cda_ctx cda_ctx;
+
+/* Detail for NS_ORDER / BYZANTINE / NS_SHORT errors (mirrors rsmt2d.ErrByzantineData
+ * and nmt's push-order error: which axis/index and which leaf). */
+typedef struct {
+  int32_t code;
+  int32_t axis;  /* CDA_AXIS_ROW / CDA_AXIS_COL, or -1 */
+  int32_t index; /* axis index, or -1 */
+  int32_t leaf;  /* leaf (share) index within the axis, or -1 */
+  int32_t block; /* block index within a batch, or -1 */
+} cda_err_info;
+
+/* ---- context ---------------------------------------------------------- */
+/* Creates a context bound to HIP device `device` (one process per GPU). */
+int cda_init(int device, cda_ctx** out);
+void cda_free(cda_ctx* ctx);
+const char* cda_strerror(int code);
+/* Last HIP error string recorded by the context (for CDA_E_DEVICE). */
+const char* cda_last_device_error(cda_ctx* ctx);
+
+/* ---- rsmt2d.Codec (LeoRSCodec replacement) ---------------------------- */
+/* Replaces rsmt2d.LeoRSCodec selected by appconsts.DefaultCodec
+ * (pkg/appconsts/global_consts.go:92).  Leopard GF(2^8) for 2k <= 256, GF(2^16) above. */
+/* Codec.Encode(data [][]byte) ([][]byte, error): k data shards (contiguous,
+ * k*shard_len bytes) -> k parity shards (k*shard_len). */
+int cda_rs_encode(cda_ctx* ctx, uint32_t k, uint32_t shard_len, const uint8_t* data, uint8_t* parity);
+/* Codec.Decode(shards [][]byte) ([][]byte, error): shards = 2k*shard_len bytes
+ * (data then parity), present[i] != 0 marks available shards; missing shards are
+ * reconstructed in place.  CDA_E_TOO_FEW if fewer than k are present. */
+int cda_rs_decode(cda_ctx* ctx, uint32_t k, uint32_t shard_len, uint8_t* shards, const uint8_t* present);
+/* Codec.MaxChunks() */
+int64_t cda_rs_max_chunks(void);
+/* Codec.Name() -> "Leopard" */
+const char* cda_rs_name(void);
+/* Codec.ValidateChunkSize(int) error */
+int cda_rs_validate_chunk_size(int64_t chunk_size);
+
+/* ---- block path: da.ExtendShares + da.NewDataAvailabilityHeader -------- */
+/* Replaces da.ExtendShares (pkg/da/data_availability_header.go:65-75) followed by
+ * da.NewDataAvailabilityHeader (:44-63) and DataAvailabilityHeader.Hash (:92-108).
+ * shares: `count` shares of share_len bytes, row-major ODS (count must be a
+ * power of two and a perfect square, k = sqrt(count)).
+ * eds_or_null: 4k^2*share_len bytes row-major EDS, or NULL to skip the copy-out.
+ * row_roots / col_roots: 2k*90 bytes each.  dah: 32 bytes. */
+int cda_extend_commit(cda_ctx* ctx, uint32_t count, uint32_t share_len, const uint8_t* shares,
+                      uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                      cda_err_info* err);
+
+/* Batched form: nblocks independent ODS of k*k shares each, stride k*k*share_len;
+ * outputs strided the same way (eds: 4k^2*share_len per block, roots 2k*90, dah 32). */
+int cda_extend_commit_batch(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const uint8_t* ods,
+                            uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                            cda_err_info* err);
+
+/* Device-resident form (pointers are device memory of this ctx's GPU; `stream`
+ * is a hipStream_t or NULL for the null stream).  Asynchronous: returns after
+ * enqueueing; namespace-order errors are reported into the device word
+ * `d_status` (int32 per block: 0 ok, else CDA_E_NS_ORDER) for the caller to read.
+ * d_roots: nblocks * 4k * 96 bytes (row roots then col roots, 90-B node + 6 zero
+ * bytes per record).  d_dah: nblocks * 32. */
+int cda_extend_commit_device(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds,
+                             void* d_roots, void* d_dah, void* d_status, void* stream);
+
+/* Roots + DAH of an existing EDS (rsmt2d eds.RowRoots/ColRoots + DAH hash). */
+int cda_commit_eds(cda_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots,
+                   uint8_t* dah, cda_err_info* err);
+
+/* DataAvailabilityHeader.Hash() over given roots (RFC-6962, go-square/merkle
+ * HashFromByteSlices over rowRoots ‖ colRoots; n roots per axis, 90 B each). */
+int cda_dah_hash(cda_ctx* ctx, uint32_t n, const uint8_t* row_roots, const uint8_t* col_roots, uint8_t* dah);
+
+/* ---- wrapper.NewConstructor tree (rsmt2d.TreeConstructorFn) ------------ */
+/* Root of one erasured NMT axis: replaces ErasuredNamespacedMerkleTree
+ * Push x n + Root (pkg/wrapper/nmt_wrapper.go:93-124) for square size k and
+ * axis index `axis_index`.  leaves: n * leaf_len bytes. */
+int cda_nmt_axis_root(cda_ctx* ctx, uint64_t square_size, uint64_t axis_index, uint32_t n, uint32_t leaf_len,
+                      const uint8_t* leaves, uint8_t* root, cda_err_info* err);
+
+/* ---- rsmt2d Repair ------------------------------------------------------ */
+/* Replaces (*rsmt2d.ExtendedDataSquare).Repair(rowRoots, colRoots): eds is the
+ * 4k^2*share_len square with missing cells marked by present[r*2k+c] == 0;
+ * repaired in place (present updated).  Returns CDA_OK, CDA_E_UNREPAIRABLE or
+ * CDA_E_BYZANTINE (err->axis/index). */
+int cda_repair(cda_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+               const uint8_t* col_roots, cda_err_info* err);
+
+/* ---- instrumentation ----------------------------------------------------- */
+/* When enabled, every kernel launch is bracketed by HIP events on its own
+ * stream and per-kernel total time / launch counts are accumulated. */
+int cda_profile_enable(cda_ctx* ctx, int enable);
+/* Copies up to `cap` entries: names (NUL-separated into names_buf), total ms, launches. */
+int cda_profile_read(cda_ctx* ctx, char* names_buf, size_t names_cap, double* total_ms, int64_t* launches,
+                     int cap);
+int cda_profile_reset(cda_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -19,6 +19,7 @@ NODE = 90
 
 OK, E_NOT_POW2, E_NOT_SQUARE, E_SHARD_SIZE, E_NS_SHORT, E_NS_ORDER, E_TOO_FEW, \
     E_UNREPAIRABLE, E_BYZANTINE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+E_PUSH_PAST = -11
 
 
 def lib():

@@ -1,0 +1,61 @@
+"""CPU tests of the C-ABI boundary: libcda.so loads and exports every symbol of include/cda.h.
+
+No compute is called here (no GPU in the build container).
+"""
+import os
+import re
+
+import cda
+from cda import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "cda.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cda_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_what_binding_binds():
+    assert header_functions() == sorted(N.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = cda.lib()
+    for name in header_functions():
+        assert hasattr(L, name), name
+
+
+def test_pure_host_entry_points():
+    L = cda.lib()
+    assert L.cda_rs_name() == b"Leopard"
+    assert L.cda_rs_max_chunks() == 32768 * 32768
+    assert L.cda_rs_validate_chunk_size(512) == 0
+    assert L.cda_rs_validate_chunk_size(100) == N.E_SHARD_SIZE
+    assert N.strerror(N.E_NS_ORDER).startswith("pushed data")
+
+
+def test_error_codes_match_header():
+    src = open(os.path.join(ROOT, "include", "cda.h")).read()
+    codes = dict((m[0], int(m[1])) for m in re.findall(r"(CDA_E_[A-Z0-9_]+)\s*=\s*(-?\d+)", src))
+    for name, val in codes.items():
+        assert getattr(N, name[4:]) == val, name
+
+
+def test_wrapper_push_errors_without_gpu():
+    # push-time checks mirror nmt_wrapper.go:93-114 and need no device
+    from cda.wrapper import ErasuredNamespacedMerkleTree, PushError
+    import pytest
+    t = ErasuredNamespacedMerkleTree(16, 0)
+    with pytest.raises(PushError):
+        t.push(b"\x01")
+    t = ErasuredNamespacedMerkleTree(2, 0)
+    for _ in range(4):
+        t.push(b"\x00" * 512)
+    with pytest.raises(PushError):
+        t.push(b"\x00" * 512)
+    t = ErasuredNamespacedMerkleTree(4, 0)
+    t.push(b"\x01" * 512)
+    with pytest.raises(PushError):
+        t.push(b"\x00" * 512)

@@ -1,0 +1,148 @@
+"""GPU parity: libcda (HIP, gfx950) vs the CPU oracle and the reference's KATs.
+
+Every comparison is bit-exact (integer / byte / GF arithmetic; no tolerance).
+"""
+import numpy as np
+import pytest
+
+import kat
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+# ---- reference known answers through the product path ----------------------------------
+def test_min_data_availability_header(ctx):
+    from cda import da
+    dah = da.min_data_availability_header()
+    assert dah.hash() == kat.MIN_DAH
+    dah.validate_basic()
+
+
+@pytest.mark.parametrize("k,expected", [(2, kat.TYPICAL_K2), (128, kat.MAX_K128)])
+def test_new_data_availability_header(ctx, k, expected):
+    from cda import da
+    shares = [bytes(s) for s in kat.generate_shares(k * k)]
+    eds = da.extend_shares(shares)
+    got = da.new_data_availability_header(eds)
+    assert len(got.row_roots) == 2 * k and len(got.column_roots) == 2 * k
+    assert got.hash() == expected
+
+
+def test_nil_dah_hash(ctx):
+    from cda import da
+    assert da.DataAvailabilityHeader().hash() == kat.EMPTY_HASH
+
+
+@pytest.mark.parametrize("count", [5, 129 * 129])
+def test_extend_shares_errors(ctx, count):
+    from cda import da
+    with pytest.raises(Exception):
+        da.extend_shares([bytes(s) for s in kat.generate_shares(count)])
+
+
+# ---- seeded random squares vs the oracle ---------------------------------------------------
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128])
+def test_extend_commit_matches_oracle(ctx, k):
+    ods = O.gen_ods(k, 0xC0FFEE + k)
+    rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods)
+    assert rc == 0
+    eds, rr, cr, dah = ctx.extend_commit(ods)
+    assert np.array_equal(eds, eds_o), "EDS bytes differ"
+    assert np.array_equal(rr, rr_o), "row roots differ"
+    assert np.array_equal(cr, cr_o), "col roots differ"
+    assert dah == dah_o
+
+
+def test_batch_matches_single(ctx):
+    k, nb = 32, 6
+    ods = np.stack([O.gen_ods(k, 0xC0FFEE + b) for b in range(nb)])
+    eds, rr, cr, dah = ctx.extend_commit_batch(ods)
+    for b in range(nb):
+        rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods[b])
+        assert np.array_equal(eds[b], eds_o) and np.array_equal(rr[b], rr_o) and np.array_equal(cr[b], cr_o)
+        assert dah[b].tobytes() == dah_o
+
+
+def test_random_bytes_not_sorted_rows_are_rejected(ctx):
+    from cda import CdaError
+    k = 8
+    ods = O.gen_ods(k, 99)
+    ods[[3, 5]] = ods[[5, 3]]  # row 0: leaf 3 > leaf 4 after the swap
+    with pytest.raises(CdaError) as ei:
+        ctx.extend_commit(ods)
+    assert ei.value.code == -5 and ei.value.axis == 0 and ei.value.index == 0
+
+
+def test_column_order_violation(ctx):
+    from cda import CdaError
+    k = 4
+    ods = O.gen_ods(k, 98).reshape(k, k, 512).copy()
+    # make column 2 decrease between rows 1 and 2 while keeping every row sorted
+    ods[2, :, 19:29] = 0
+    ods[2, :, 29:] = 0
+    ods[3, :, 19:29] = 0
+    rows_sorted = np.sort(ods.reshape(k * k, 512).view("S512").reshape(k, k), axis=1)
+    ods = rows_sorted.view(np.uint8).reshape(k * k, 512)
+    rc, *_ = O.extend_commit(ods)
+    with pytest.raises(CdaError) as ei:
+        ctx.extend_commit(ods)
+    assert ei.value.code == -5
+
+
+# ---- codec ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 7, 8, 15, 16, 33, 64, 100, 127, 128])
+@pytest.mark.parametrize("L", [64, 512, 1024])
+def test_rs_encode_matches_oracle(ctx, k, L):
+    rng = np.random.default_rng(k * 1000 + L)
+    d = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    assert np.array_equal(ctx.rs_encode(d), O.leo_encode(d))
+
+
+def test_codec_interface(ctx):
+    from cda.rsmt2d import LeoRSCodec
+    c = LeoRSCodec(ctx)
+    assert c.name() == "Leopard" and c.max_chunks() == 32768 * 32768
+    data = [bytes([i]) * 512 for i in range(4)]
+    par = c.encode(data)
+    assert par == [bytes(p) for p in O.leo_encode(np.stack([np.frombuffer(d, np.uint8) for d in data]))]
+
+
+# ---- trees ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("k,axis,n", [(8, 0, 16), (8, 3, 16), (8, 9, 16), (8, 0, 8), (8, 0, 5), (128, 0, 256),
+                                      (4, 1, 1), (1, 0, 2)])
+def test_axis_root_matches_oracle(ctx, k, axis, n):
+    ods = O.gen_ods(max(k, 4), k + axis + n)
+    leaves = [bytes(ods[i % len(ods)]) for i in range(n)]
+    leaves[:min(n, k)] = sorted(leaves[:min(n, k)])
+    rc, want, _ = O.nmt_axis_root(k, axis, leaves)
+    assert rc == 0
+    assert ctx.nmt_axis_root(k, axis, leaves) == want
+
+
+def test_wrapper_tree_roots(ctx):
+    from cda.wrapper import new_constructor
+    k = 8
+    rc, eds, rr, cr, _ = O.extend_commit(O.gen_ods(k, 5))
+    eds = eds.reshape(2 * k, 2 * k, 512)
+    ctor = new_constructor(k, ctx)
+    for r in (0, 5, 8, 15):
+        t = ctor(0, r)
+        for c in range(2 * k):
+            t.push(bytes(eds[r, c]))
+        assert t.root() == bytes(rr[r])
+
+
+def test_empty_tree_root(ctx):
+    from cda.wrapper import ErasuredNamespacedMerkleTree
+    r1 = ErasuredNamespacedMerkleTree(1, 0, ctx).root()
+    r2 = ErasuredNamespacedMerkleTree(2, 1, ctx).root()
+    assert r1 == r2 and r1[58:] == kat.EMPTY_HASH
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 6, 7, 256, 1000])
+def test_dah_hash_any_count(ctx, n):
+    rng = np.random.default_rng(n)
+    rr = rng.integers(0, 256, (n, 90), dtype=np.uint8)
+    cr = rng.integers(0, 256, (n, 90), dtype=np.uint8)
+    assert ctx.dah_hash(rr, cr) == O.dah_hash(rr, cr)
