@@ -27,6 +27,8 @@ namespace cda {
 
 __constant__ uint16_t c_skew8[256];
 __constant__ unsigned long long c_col8[256];
+// 0/~0 mask words, entry [L][j*8+b] = bit j of (1<<b)*exp(L); constant address space => s_load into SGPRs
+__constant__ uint32_t c_masks8[256 * 64];
 
 // --- bit slicing -----------------------------------------------------------
 // 8 words (32 bytes, little-endian) <-> 8 planes; plane j bit (8b+i) = bit j of
@@ -175,8 +177,164 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
   }
 }
 
+// ===========================================================================
+// Register-resident encoder: 4 codewords x 16 units per workgroup.
+//
+// Lane l of every wave owns (codeword l/16, 32-byte unit l%16) and holds 16
+// elements of that column in registers (16 x 8 plane words).  All 64 lanes of
+// a wave hold the SAME element indices, so every butterfly constant is
+// wave-uniform: its 8x8 GF(2) mask matrix is fetched with scalar loads into
+// SGPRs and x ^= M*y is 64 v_bitop3 with an SGPR operand.  Layers on index
+// bits {f..f+3} run in registers; changing f is one LDS exchange (128 KiB).
+//   m = 2^L, L in 4..7:  IFFT bits 0..3 (f=0) | exchange | IFFT bits 4..L-1 and
+//   FFT bits L-1..L-4 (f=L-4) | exchange | FFT bits L-5..0 (f=0).
+// ===========================================================================
+struct Rs8RegArgs {
+  const uint8_t* src;
+  long long src_blk, src_cw, src_sh;
+  uint8_t* dst;
+  long long dst_blk, dst_cw, dst_sh;
+  uint8_t* cpy;
+  long long cpy_blk, cpy_cw, cpy_sh;
+  const uint32_t* masks;  // [256][64] 0/~0 words: entry j*8+b = bit j of (1<<b)*exp(L)
+  int k, groups_per_blk, slices;
+};
+
+template <bool INVERSE>
+__device__ __forceinline__ void bfly_u(uint32_t (&X)[8], uint32_t (&Y)[8], int sidx, const uint32_t* __restrict__ masks) {
+  const unsigned lm = c_skew8[sidx];
+  if (INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+  }
+  if (lm != 255u) {
+    const uint32_t* mk = c_masks8 + lm * 64;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint32_t acc = X[j];
+#pragma unroll
+      for (int b = 0; b < 8; b++) acc = __builtin_amdgcn_bitop3_b32(acc, Y[b], mk[j * 8 + b], 0x78);
+      X[j] = acc;
+    }
+  }
+  if (!INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+  }
+}
+
+// element index of register r for wave w in layout f (4 register bits at f..f+3)
+__device__ __forceinline__ int x_of(int w, int r, int f) {
+  return ((w >> f) << (f + 4)) | (r << f) | (w & ((1 << f) - 1));
+}
+
+template <bool INVERSE, int M>
+__device__ __forceinline__ void layer_u(uint32_t (&E)[16][8], int w, int f, int d, const uint32_t* masks) {
+  const int rb = d - f;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    if (r & (1 << rb)) continue;
+    const int x = x_of(w, r, f);
+    const int s0 = (x >> (d + 1)) << (d + 1);
+    const int idx = INVERSE ? (M - 1 + s0 + (1 << d)) : (s0 + (1 << d) - 1);
+    bfly_u<INVERSE>(E[r], E[r | (1 << rb)], idx, masks);
+  }
+}
+
+template <int M>
+__device__ __forceinline__ void exchange(uint32_t (&E)[16][8], uint4* xbuf, int w, int lane, int f_from, int f_to) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int x = x_of(w, r, f_from);
+      xbuf[x * 64 + lane] = make_uint4(E[r][4 * h], E[r][4 * h + 1], E[r][4 * h + 2], E[r][4 * h + 3]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int x = x_of(w, r, f_to);
+      const uint4 v = xbuf[x * 64 + lane];
+      E[r][4 * h] = v.x;
+      E[r][4 * h + 1] = v.y;
+      E[r][4 * h + 2] = v.z;
+      E[r][4 * h + 3] = v.w;
+    }
+    __syncthreads();
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(64 << (L - 4)) rs_encode8_reg_kernel(Rs8RegArgs a) {
+  constexpr int M = 1 << L;
+  constexpr int NW = 1 << (L - 4);
+  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];  // [M][64] (L > 4 only)
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & (NW - 1);
+  const int cwi = lane >> 4, u = lane & 15;
+  int wg = blockIdx.x;
+  const int slice = wg % a.slices;
+  wg /= a.slices;
+  const int grp = wg % a.groups_per_blk;
+  const int blk = wg / a.groups_per_blk;
+  const int cw = grp * 4 + cwi;
+  const long long off = (long long)slice * 512 + u * 32;
+  const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
+  uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
+  uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
+  const uint32_t* __restrict__ masks = a.masks;
+
+  uint32_t E[16][8];
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int x = x_of(w, r, 0);
+    if (x < a.k) {
+      const uint4* p = reinterpret_cast<const uint4*>(src + x * a.src_sh);
+      const uint4 v0 = p[0], v1 = p[1];
+      if (cpy) {
+        uint4* q = reinterpret_cast<uint4*>(cpy + x * a.cpy_sh);
+        q[0] = v0;
+        q[1] = v1;
+      }
+      E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
+      E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
+      bitslice8(E[r]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j++) E[r][j] = 0;
+    }
+  }
+  // IFFT bits 0..3
+#pragma unroll
+  for (int d = 0; d < 4; d++) layer_u<true, M>(E, w, 0, d, masks);
+  constexpr int F2 = L - 4;
+  if (L > 4) exchange<M>(E, xbuf, w, lane, 0, F2);
+  // IFFT bits 4..L-1, FFT bits L-1..F2
+#pragma unroll
+  for (int d = 4; d < L; d++) layer_u<true, M>(E, w, F2, d, masks);
+#pragma unroll
+  for (int d = L - 1; d >= F2; d--) layer_u<false, M>(E, w, F2, d, masks);
+  if (L > 4) exchange<M>(E, xbuf, w, lane, F2, 0);
+  // FFT bits F2-1..0
+#pragma unroll
+  for (int d = F2 - 1; d >= 0; d--) layer_u<false, M>(E, w, 0, d, masks);
+  // parity = work[0..k)
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int x = x_of(w, r, 0);
+    if (x < a.k) {
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = E[r][j];
+      bitslice8(v);
+      uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
+      q[0] = make_uint4(v[0], v[1], v[2], v[3]);
+      q[1] = make_uint4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
 int rs_init_device_tables(int device) {
-  (void)device;
   const LeoTables& t = leo_tables(8);
   uint16_t skew[256];
   unsigned long long col[256];
@@ -188,6 +346,19 @@ int rs_init_device_tables(int device) {
   if (hipFuncSetAttribute((const void*)rs_encode8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
       hipSuccess)
     return -1;
+  const void* regk[4] = {(const void*)rs_encode8_reg_kernel<4>, (const void*)rs_encode8_reg_kernel<5>,
+                         (const void*)rs_encode8_reg_kernel<6>, (const void*)rs_encode8_reg_kernel<7>};
+  for (auto f : regk)
+    if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) != hipSuccess) return -1;
+  {
+    uint32_t* host = new uint32_t[256 * 64];
+    for (unsigned l = 0; l < 256; l++)
+      for (int j = 0; j < 8; j++)
+        for (int b = 0; b < 8; b++) host[l * 64 + j * 8 + b] = ((col[l] >> (8 * b + j)) & 1) ? 0xFFFFFFFFu : 0u;
+    const bool ok = hipMemcpyToSymbol(HIP_SYMBOL(c_masks8), host, 256 * 64 * 4) == hipSuccess;
+    delete[] host;
+    if (!ok) return -1;
+  }
   return 0;
 }
 
@@ -199,6 +370,36 @@ static int ilog2(int v) {
 
 int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   if (j.k < 1 || j.k > 128 || j.shard_len % 64 != 0) return -2;
+  const int L = ilog2(j.k);
+  if (L >= 4 && j.cw_per_blk % 4 == 0 && j.shard_len % 512 == 0) {
+    Rs8RegArgs r;
+    r.src = j.src;
+    r.src_blk = j.src_blk;
+    r.src_cw = j.src_cw;
+    r.src_sh = j.src_sh;
+    r.dst = j.dst;
+    r.dst_blk = j.dst_blk;
+    r.dst_cw = j.dst_cw;
+    r.dst_sh = j.dst_sh;
+    r.cpy = j.cpy;
+    r.cpy_blk = j.cpy_blk;
+    r.cpy_cw = j.cpy_cw;
+    r.cpy_sh = j.cpy_sh;
+    r.masks = nullptr;
+    r.k = j.k;
+    r.groups_per_blk = j.cw_per_blk / 4;
+    r.slices = j.shard_len / 512;
+    const long long grid = (long long)j.nblk * r.groups_per_blk * r.slices;
+    const size_t lds = L > 4 ? (size_t)(1 << L) * 64 * 16 : 0;
+    const dim3 block(64 << (L - 4));
+    switch (L) {
+      case 4: hipLaunchKernelGGL(rs_encode8_reg_kernel<4>, dim3((unsigned)grid), block, lds, s, r); break;
+      case 5: hipLaunchKernelGGL(rs_encode8_reg_kernel<5>, dim3((unsigned)grid), block, lds, s, r); break;
+      case 6: hipLaunchKernelGGL(rs_encode8_reg_kernel<6>, dim3((unsigned)grid), block, lds, s, r); break;
+      default: hipLaunchKernelGGL(rs_encode8_reg_kernel<7>, dim3((unsigned)grid), block, lds, s, r); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   Rs8Args a;
   a.src = j.src;
   a.src_blk = j.src_blk;
