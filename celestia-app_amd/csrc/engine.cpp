@@ -13,7 +13,9 @@
 // buffers and maps device status words to error codes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -27,6 +29,13 @@ struct cda_ctx {
   int device = 0;
   std::recursive_mutex mu;
   hipStream_t stream = nullptr;
+  // sub-batch streams: independent blocks of one call are split across these so
+  // that one sub-batch's memory-bound RS phase and latency-bound tree tail overlap
+  // another's hashing (no dependency between blocks).
+  static constexpr int kMaxSub = 8;
+  int nsub = 4;
+  hipStream_t sub[kMaxSub] = {};
+  hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::string last_err;
   // workspace
   struct Buf {
@@ -108,6 +117,8 @@ void flush_profile(cda_ctx* c) {
   c->pending.clear();
 }
 
+void* bufs0(cda_ctx* c, size_t rec_off) { return (uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES; }
+
 int ilog2i(uint32_t v) {
   int l = 0;
   while ((1u << l) < v) l++;
@@ -124,15 +135,11 @@ void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block
   e->block = block;
 }
 
-// Enqueue the whole block pipeline.  d_roots: nblocks * 4k records (96 B).
-int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
-                     void* d_dah, unsigned long long* d_status, hipStream_t s) {
+// Enqueue the whole block pipeline for blocks [0, nblocks) of the given buffers,
+// using leaf/scratch records starting at record offset `rec_off`.
+int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
+                         void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
   const uint32_t w = 2 * k;
-  const size_t cells = (size_t)nblocks * w * w;
-  int rc = ensure(c, c->leaf, cells * CDA_REC_BYTES);
-  if (rc) return rc;
-  rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
-  if (rc) return rc;
   const long long S = CDA_SHARE;
   {
     RsJob j{};
@@ -176,10 +183,10 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
   {
     ProfScope ps(c, "leaf_hash", s);
-    if (launch_leaf_hash(d_eds, c->leaf.p, d_status, (int)k, (int)nblocks, s)) return CDA_E_DEVICE;
+    if (launch_leaf_hash(d_eds, bufs0(c, rec_off), d_status, (int)k, (int)nblocks, s)) return CDA_E_DEVICE;
   }
   const int L = ilog2i(w);
-  void* bufs[2] = {c->leaf.p, c->scratch.p};
+  void* bufs[2] = {(uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES, (uint8_t*)c->scratch.p + rec_off * CDA_REC_BYTES};
   for (int level = 1; level <= L; level++) {
     const void* in = bufs[(level - 1) & 1];
     void* out = level == L ? d_roots : bufs[level & 1];
@@ -189,6 +196,36 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   {
     ProfScope ps(c, "dah", s);
     if (launch_dah(d_roots, d_dah, (int)(2 * w), (int)nblocks, s)) return CDA_E_DEVICE;
+  }
+  return CDA_OK;
+}
+
+// Pipeline over nblocks: split into up to c->nsub sub-batches on internal
+// streams forked from / joined back into `s` (serial when profiling so that the
+// per-kernel event timings are not overlapped).
+int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
+                     void* d_dah, unsigned long long* d_status, hipStream_t s) {
+  const uint32_t w = 2 * k;
+  const size_t cells = (size_t)nblocks * w * w;
+  int rc = ensure(c, c->leaf, cells * CDA_REC_BYTES);
+  if (rc) return rc;
+  rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
+  if (rc) return rc;
+  const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
+  if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
+  if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
+  uint32_t done = 0;
+  for (int i = 0; i < nsub; i++) {
+    const uint32_t nb = (nblocks - done) / (uint32_t)(nsub - i);
+    if (!dev_ok(c, hipStreamWaitEvent(c->sub[i], c->fork_ev, 0), "hipStreamWaitEvent")) return CDA_E_DEVICE;
+    rc = enqueue_pipeline_one(c, k, nb, d_ods + (size_t)done * k * k * CDA_SHARE, d_eds + (size_t)done * w * w * CDA_SHARE,
+                              (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES, (uint8_t*)d_dah + (size_t)done * 32,
+                              d_status + done, c->sub[i], (size_t)done * w * w);
+    if (rc) return rc;
+    if (!dev_ok(c, hipEventRecord(c->join_ev[i], c->sub[i]), "hipEventRecord") ||
+        !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[i], 0), "hipStreamWaitEvent"))
+      return CDA_E_DEVICE;
+    done += nb;
   }
   return CDA_OK;
 }
@@ -226,6 +263,15 @@ int cda_init(int device, cda_ctx** out) {
     delete c;
     return CDA_E_DEVICE;
   }
+  if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
+  bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
+    ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    delete c;
+    return CDA_E_DEVICE;
+  }
   *out = c;
   return CDA_OK;
 }
@@ -240,6 +286,11 @@ void cda_free(cda_ctx* c) {
       if (b->p) (void)hipFree(b->p);
     if (c->host_status.p) (void)hipHostFree(c->host_status.p);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < cda_ctx::kMaxSub; i++) {
+      if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
+      if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
+    }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;

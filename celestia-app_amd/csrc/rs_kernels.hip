@@ -12,12 +12,13 @@
 //
 // MI355X design: GF(2^8) multiplication by a constant is GF(2)-linear, so the
 // 32 bytes a lane owns are bit-sliced into 8 plane words (bit j of 32 bytes per
-// word) and x ^= c*y becomes 64 v_bitop3 (acc ^ (y_b & mask_jb)) per 32 bytes,
-// no tables in the inner loop.  The mask matrix of each butterfly constant comes
-// from an 8-byte column table in constant memory; when all lanes of a wave share
-// the constant (D*U >= 64) it is read through readfirstlane so the masks live in
-// SGPRs (SALU), otherwise per lane.  One workgroup owns one codeword x 16 units
-// (the whole 512-B shard); the m x 512-B state stays in LDS for all 2*log2(m) layers.
+// word) and butterflies are whole-register XORs.  Two kernels:
+//  * rs_encode8_g2_kernel (batched EDS path): 2 codewords per workgroup held in
+//    registers, lane index bit 0 of the element index, wave-uniform constants,
+//    multiply in the standard polynomial basis (x^8+x^4+x^3+x^2+1) by uniform
+//    branches over the constant's bits -- full-rate v_xor only.
+//  * rs_encode8_kernel (single codewords / small k / odd shard lengths): state
+//    in LDS, radix-2 layers, constant matrix applied with v_bitop3 masks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,8 +28,6 @@ namespace cda {
 
 __constant__ uint16_t c_skew8[256];
 __constant__ unsigned long long c_col8[256];
-// 0/~0 mask words, entry [L][j*8+b] = bit j of (1<<b)*exp(L); constant address space => s_load into SGPRs
-__constant__ uint32_t c_masks8[256 * 64];
 
 // --- bit slicing -----------------------------------------------------------
 // 8 words (32 bytes, little-endian) <-> 8 planes; plane j bit (8b+i) = bit j of
@@ -177,18 +176,72 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
   }
 }
 
-// ===========================================================================
-// Register-resident encoder: 4 codewords x 16 units per workgroup.
-//
-// Lane l of every wave owns (codeword l/16, 32-byte unit l%16) and holds 16
-// elements of that column in registers (16 x 8 plane words).  All 64 lanes of
-// a wave hold the SAME element indices, so every butterfly constant is
-// wave-uniform: its 8x8 GF(2) mask matrix is fetched with scalar loads into
-// SGPRs and x ^= M*y is 64 v_bitop3 with an SGPR operand.  Layers on index
-// bits {f..f+3} run in registers; changing f is one LDS exchange (128 KiB).
-//   m = 2^L, L in 4..7:  IFFT bits 0..3 (f=0) | exchange | IFFT bits 4..L-1 and
-//   FFT bits L-1..L-4 (f=L-4) | exchange | FFT bits L-5..0 (f=0).
-// ===========================================================================
+// ---- polynomial-basis arithmetic --------------------------------------------
+// Leopard's byte e is the Cantor-basis coordinate vector of phi(e) in the standard
+// field GF(2)[x]/(x^8+x^4+x^3+x^2+1), and exp(L) maps to alpha^L (alpha = x):
+//   mul_leopard(a, b) = phi^-1(phi(a) * phi(b))      (checked in tests/test_oracle.py).
+// In the standard basis, multiplying 8 bit-planes by alpha is a plane rotation
+// plus 3 XORs, so x ^= c*y = XOR_{i: c_i} alpha^i*y costs 21 + 8*popcount(c)
+// full-rate v_xor with wave-uniform branches on c's bits -- no SGPR operands
+// (measured: VALU ops with an SGPR source issue at half rate on gfx950,
+// tools/valu_ubench.hip).
+__constant__ uint8_t c_cpoly8[256];  // per skew index: alpha^skew in std basis, 0 = no multiply
+
+constexpr uint8_t kPhi8[8] = {1, 214, 152, 146, 86, 200, 88, 230};     // columns: phi(1<<j)
+constexpr uint8_t kPhiInv8[8] = {1, 104, 92, 100, 114, 240, 86, 18};  // columns: phi^-1(1<<j)
+
+__device__ __forceinline__ void apply8(uint32_t (&v)[8], const uint8_t (&cols)[8]) {
+  uint32_t o[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if ((cols[j] >> i) & 1) acc ^= v[j];
+    o[i] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = o[i];
+}
+
+// X ^= c * Y in the standard basis; c is wave-uniform.
+__device__ __forceinline__ void gf8_muladd_poly(uint32_t (&X)[8], const uint32_t (&Y)[8], unsigned c) {
+  uint32_t T[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) T[j] = Y[j];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (c & (1u << i)) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) X[j] ^= T[j];
+    }
+    if (i < 7) {  // T *= alpha; unconditional so T's registers are renamed statically
+      const uint32_t t = T[7];
+      T[7] = T[6];
+      T[6] = T[5];
+      T[5] = T[4];
+      T[4] = T[3] ^ t;
+      T[3] = T[2] ^ t;
+      T[2] = T[1] ^ t;
+      T[1] = T[0];
+      T[0] = t;
+    }
+  }
+}
+
+template <bool INVERSE>
+__device__ __forceinline__ void bfly_p(uint32_t (&X)[8], uint32_t (&Y)[8], unsigned c) {
+  if (INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+  }
+  if (c != 0u) gf8_muladd_poly(X, Y, c);
+  if (!INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+  }
+}
+
 struct Rs8RegArgs {
   const uint8_t* src;
   long long src_blk, src_cw, src_sh;
@@ -196,65 +249,88 @@ struct Rs8RegArgs {
   long long dst_blk, dst_cw, dst_sh;
   uint8_t* cpy;
   long long cpy_blk, cpy_cw, cpy_sh;
-  const uint32_t* masks;  // [256][64] 0/~0 words: entry j*8+b = bit j of (1<<b)*exp(L)
   int k, groups_per_blk, slices;
 };
 
-template <bool INVERSE>
-__device__ __forceinline__ void bfly_u(uint32_t (&X)[8], uint32_t (&Y)[8], int sidx, const uint32_t* __restrict__ masks) {
-  const unsigned lm = c_skew8[sidx];
-  if (INVERSE) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
-  }
-  if (lm != 255u) {
-    const uint32_t* mk = c_masks8 + lm * 64;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      uint32_t acc = X[j];
-#pragma unroll
-      for (int b = 0; b < 8; b++) acc = __builtin_amdgcn_bitop3_b32(acc, Y[b], mk[j * 8 + b], 0x78);
-      X[j] = acc;
-    }
-  }
-  if (!INVERSE) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
-  }
-}
-
-// element index of register r for wave w in layout f (4 register bits at f..f+3)
-__device__ __forceinline__ int x_of(int w, int r, int f) {
-  return ((w >> f) << (f + 4)) | (r << f) | (w & ((1 << f) - 1));
+// ===========================================================================
+// Two-codeword register encoder (default): 2 codewords x 16 units per workgroup,
+// 8 elements per lane, so a workgroup holds 128 KiB of state and two
+// workgroups fit on a CU (one streams HBM while the other computes).
+//
+// Lane l: unit l&15, codeword (l>>4)&1, and index bit 0 of its elements = l>>5
+// ("sw").  Every other index bit is a register bit (3 per layout) or a wave bit,
+// so for any layer d >= 1 the butterfly partner is in the same lane and the
+// constant (a function of index bits > d) is wave-uniform: SGPR masks.  Layer
+// d = 0 pairs lanes l and l^32: both halves form T = x ^ y; the x half then adds
+// M*T (wave-uniform constant as well).
+//   P1 f=1: IFFT d=0 (cross-lane), d=1..3 | exchange | P2 f=L-3: IFFT d=4..L-1,
+//   FFT d=L-1..L-3 | exchange | P3 f=1: FFT d=min(3,L-4)..1, d=0 (cross-lane).
+// ===========================================================================
+__device__ __forceinline__ int x2_of(int w, int sw, int r, int f) {
+  // bits 1..L-1 of the element index: 3 register bits at (f..f+2), wave bits elsewhere
+  const int y = ((w >> (f - 1)) << (f + 2)) | (r << (f - 1)) | (w & ((1 << (f - 1)) - 1));
+  return (y << 1) | sw;
 }
 
 template <bool INVERSE, int M>
-__device__ __forceinline__ void layer_u(uint32_t (&E)[16][8], int w, int f, int d, const uint32_t* masks) {
+__device__ __forceinline__ void layer2_u(uint32_t (&E)[8][8], int w, int f, int d) {
   const int rb = d - f;
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
+  for (int r = 0; r < 8; r++) {
     if (r & (1 << rb)) continue;
-    const int x = x_of(w, r, f);
+    const int x = x2_of(w, 0, r, f);
     const int s0 = (x >> (d + 1)) << (d + 1);
     const int idx = INVERSE ? (M - 1 + s0 + (1 << d)) : (s0 + (1 << d) - 1);
-    bfly_u<INVERSE>(E[r], E[r | (1 << rb)], idx, masks);
+    bfly_p<INVERSE>(E[r], E[r | (1 << rb)], c_cpoly8[idx]);
   }
 }
 
+// d = 0 across lane halves (element x in lanes 0..31, x+1 in lanes 32..63).
+template <bool INVERSE, int M>
+__device__ __forceinline__ void layer2_d0(uint32_t (&E)[8][8], int w, int f, bool upper) {
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int x = x2_of(w, 0, r, f);
+    const unsigned c = c_cpoly8[INVERSE ? (M - 1 + x + 1) : x];
+    uint32_t P[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) P[j] = __shfl_xor(E[r][j], 32);
+    uint32_t X[8], Y[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      X[j] = upper ? P[j] : E[r][j];
+      Y[j] = upper ? E[r][j] : P[j];
+    }
+    if (INVERSE) {  // y' = x ^ y ; x' = x ^ c*y'
+#pragma unroll
+      for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+      if (c != 0u) gf8_muladd_poly(X, Y, c);
+    } else {  // x' = x ^ c*y ; y' = y ^ x'
+      if (c != 0u) gf8_muladd_poly(X, Y, c);
+#pragma unroll
+      for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) E[r][j] = upper ? Y[j] : X[j];
+  }
+}
+
+// LDS exchange of the 8 x 8 register state between layouts (two halves of 4 planes).
 template <int M>
-__device__ __forceinline__ void exchange(uint32_t (&E)[16][8], uint4* xbuf, int w, int lane, int f_from, int f_to) {
+__device__ __forceinline__ void exchange2(uint32_t (&E)[8][8], uint4* xbuf, int w, int sw, int li, int f_from,
+                                          int f_to) {
 #pragma unroll
   for (int h = 0; h < 2; h++) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const int x = x_of(w, r, f_from);
-      xbuf[x * 64 + lane] = make_uint4(E[r][4 * h], E[r][4 * h + 1], E[r][4 * h + 2], E[r][4 * h + 3]);
+    for (int r = 0; r < 8; r++) {
+      const int x = x2_of(w, sw, r, f_from);
+      xbuf[x * 32 + li] = make_uint4(E[r][4 * h], E[r][4 * h + 1], E[r][4 * h + 2], E[r][4 * h + 3]);
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const int x = x_of(w, r, f_to);
-      const uint4 v = xbuf[x * 64 + lane];
+    for (int r = 0; r < 8; r++) {
+      const int x = x2_of(w, sw, r, f_to);
+      const uint4 v = xbuf[x * 32 + li];
       E[r][4 * h] = v.x;
       E[r][4 * h + 1] = v.y;
       E[r][4 * h + 2] = v.z;
@@ -265,29 +341,29 @@ __device__ __forceinline__ void exchange(uint32_t (&E)[16][8], uint4* xbuf, int 
 }
 
 template <int L>
-__global__ void __launch_bounds__(64 << (L - 4)) rs_encode8_reg_kernel(Rs8RegArgs a) {
+__global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegArgs a) {
   constexpr int M = 1 << L;
   constexpr int NW = 1 << (L - 4);
-  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];  // [M][64] (L > 4 only)
+  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];  // [M][32] x 16 B (L > 4 only)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & (NW - 1);
-  const int cwi = lane >> 4, u = lane & 15;
+  const int u = lane & 15, cwi = (lane >> 4) & 1, sw = lane >> 5, li = lane & 31;
+  const bool upper = sw != 0;
   int wg = blockIdx.x;
   const int slice = wg % a.slices;
   wg /= a.slices;
   const int grp = wg % a.groups_per_blk;
   const int blk = wg / a.groups_per_blk;
-  const int cw = grp * 4 + cwi;
+  const int cw = grp * 2 + cwi;
   const long long off = (long long)slice * 512 + u * 32;
   const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
   uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
   uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
-  const uint32_t* __restrict__ masks = a.masks;
 
-  uint32_t E[16][8];
+  uint32_t E[8][8];
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int x = x_of(w, r, 0);
+  for (int r = 0; r < 8; r++) {
+    const int x = x2_of(w, sw, r, 1);
     if (x < a.k) {
       const uint4* p = reinterpret_cast<const uint4*>(src + x * a.src_sh);
       const uint4 v0 = p[0], v1 = p[1];
@@ -299,33 +375,36 @@ __global__ void __launch_bounds__(64 << (L - 4)) rs_encode8_reg_kernel(Rs8RegArg
       E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
       E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
       bitslice8(E[r]);
+      apply8(E[r], kPhi8);  // Cantor coordinates -> standard basis
     } else {
 #pragma unroll
       for (int j = 0; j < 8; j++) E[r][j] = 0;
     }
   }
-  // IFFT bits 0..3
+  constexpr int F2 = L - 3;  // P2 register bits F2..F2+2 = L-3..L-1
+  // P1 (f=1): IFFT d=0 (cross-lane), d=1..3 (or up to L-1 when L == 4)
+  layer2_d0<true, M>(E, w, 1, upper);
 #pragma unroll
-  for (int d = 0; d < 4; d++) layer_u<true, M>(E, w, 0, d, masks);
-  constexpr int F2 = L - 4;
-  if (L > 4) exchange<M>(E, xbuf, w, lane, 0, F2);
-  // IFFT bits 4..L-1, FFT bits L-1..F2
+  for (int d = 1; d < 4 && d < L; d++) layer2_u<true, M>(E, w, 1, d);
+  if (L > 4) exchange2<M>(E, xbuf, w, sw, li, 1, F2);
+  // P2: IFFT d=4..L-1, FFT d=L-1..F2
 #pragma unroll
-  for (int d = 4; d < L; d++) layer_u<true, M>(E, w, F2, d, masks);
+  for (int d = 4; d < L; d++) layer2_u<true, M>(E, w, F2, d);
 #pragma unroll
-  for (int d = L - 1; d >= F2; d--) layer_u<false, M>(E, w, F2, d, masks);
-  if (L > 4) exchange<M>(E, xbuf, w, lane, F2, 0);
-  // FFT bits F2-1..0
+  for (int d = L - 1; d >= F2 && d >= 1; d--) layer2_u<false, M>(E, w, F2, d);
+  if (L > 4) exchange2<M>(E, xbuf, w, sw, li, F2, 1);
+  // P3 (f=1): FFT d=F2-1..1, then d=0 (cross-lane)
 #pragma unroll
-  for (int d = F2 - 1; d >= 0; d--) layer_u<false, M>(E, w, 0, d, masks);
-  // parity = work[0..k)
+  for (int d = (F2 - 1 < 3 ? F2 - 1 : 3); d >= 1; d--) layer2_u<false, M>(E, w, 1, d);
+  layer2_d0<false, M>(E, w, 1, upper);
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int x = x_of(w, r, 0);
+  for (int r = 0; r < 8; r++) {
+    const int x = x2_of(w, sw, r, 1);
     if (x < a.k) {
       uint32_t v[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) v[j] = E[r][j];
+      apply8(v, kPhiInv8);  // standard basis -> Cantor coordinates
       bitslice8(v);
       uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
       q[0] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -335,6 +414,7 @@ __global__ void __launch_bounds__(64 << (L - 4)) rs_encode8_reg_kernel(Rs8RegArg
 }
 
 int rs_init_device_tables(int device) {
+  (void)device;
   const LeoTables& t = leo_tables(8);
   uint16_t skew[256];
   unsigned long long col[256];
@@ -343,22 +423,24 @@ int rs_init_device_tables(int device) {
   for (unsigned l = 0; l < 256; l++) col[l] = leo8_colbits(l);
   if (hipMemcpyToSymbol(HIP_SYMBOL(c_skew8), skew, sizeof skew) != hipSuccess) return -1;
   if (hipMemcpyToSymbol(HIP_SYMBOL(c_col8), col, sizeof col) != hipSuccess) return -1;
+  // alpha^L in the standard basis (LFSR of x^8+x^4+x^3+x^2+1), per skew index
+  uint8_t apow[255];
+  unsigned st = 1;
+  for (int i = 0; i < 255; i++) {
+    apow[i] = (uint8_t)st;
+    st <<= 1;
+    if (st & 0x100) st ^= 0x11D;
+  }
+  uint8_t cpoly[256];
+  for (int i = 0; i < 256; i++) cpoly[i] = skew[i] >= 255 ? 0 : apow[skew[i]];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(c_cpoly8), cpoly, sizeof cpoly) != hipSuccess) return -1;
   if (hipFuncSetAttribute((const void*)rs_encode8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
       hipSuccess)
     return -1;
-  const void* regk[4] = {(const void*)rs_encode8_reg_kernel<4>, (const void*)rs_encode8_reg_kernel<5>,
-                         (const void*)rs_encode8_reg_kernel<6>, (const void*)rs_encode8_reg_kernel<7>};
-  for (auto f : regk)
-    if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) != hipSuccess) return -1;
-  {
-    uint32_t* host = new uint32_t[256 * 64];
-    for (unsigned l = 0; l < 256; l++)
-      for (int j = 0; j < 8; j++)
-        for (int b = 0; b < 8; b++) host[l * 64 + j * 8 + b] = ((col[l] >> (8 * b + j)) & 1) ? 0xFFFFFFFFu : 0u;
-    const bool ok = hipMemcpyToSymbol(HIP_SYMBOL(c_masks8), host, 256 * 64 * 4) == hipSuccess;
-    delete[] host;
-    if (!ok) return -1;
-  }
+  const void* g2k[4] = {(const void*)rs_encode8_g2_kernel<4>, (const void*)rs_encode8_g2_kernel<5>,
+                        (const void*)rs_encode8_g2_kernel<6>, (const void*)rs_encode8_g2_kernel<7>};
+  for (auto f : g2k)
+    if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) != hipSuccess) return -1;
   return 0;
 }
 
@@ -371,8 +453,9 @@ static int ilog2(int v) {
 int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   if (j.k < 1 || j.k > 128 || j.shard_len % 64 != 0) return -2;
   const int L = ilog2(j.k);
-  if (L >= 4 && j.cw_per_blk % 4 == 0 && j.shard_len % 512 == 0) {
-    Rs8RegArgs r;
+  // Batched path: 2 codewords per workgroup, register-resident (k >= 16).
+  if (L >= 4 && j.cw_per_blk % 2 == 0 && j.shard_len % 512 == 0) {
+    Rs8RegArgs r{};
     r.src = j.src;
     r.src_blk = j.src_blk;
     r.src_cw = j.src_cw;
@@ -385,21 +468,22 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
     r.cpy_blk = j.cpy_blk;
     r.cpy_cw = j.cpy_cw;
     r.cpy_sh = j.cpy_sh;
-    r.masks = nullptr;
     r.k = j.k;
-    r.groups_per_blk = j.cw_per_blk / 4;
+    r.groups_per_blk = j.cw_per_blk / 2;
     r.slices = j.shard_len / 512;
     const long long grid = (long long)j.nblk * r.groups_per_blk * r.slices;
-    const size_t lds = L > 4 ? (size_t)(1 << L) * 64 * 16 : 0;
+    if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
+    const size_t lds = L > 4 ? (size_t)(1 << L) * 32 * 16 : 0;
     const dim3 block(64 << (L - 4));
     switch (L) {
-      case 4: hipLaunchKernelGGL(rs_encode8_reg_kernel<4>, dim3((unsigned)grid), block, lds, s, r); break;
-      case 5: hipLaunchKernelGGL(rs_encode8_reg_kernel<5>, dim3((unsigned)grid), block, lds, s, r); break;
-      case 6: hipLaunchKernelGGL(rs_encode8_reg_kernel<6>, dim3((unsigned)grid), block, lds, s, r); break;
-      default: hipLaunchKernelGGL(rs_encode8_reg_kernel<7>, dim3((unsigned)grid), block, lds, s, r); break;
+      case 4: hipLaunchKernelGGL(rs_encode8_g2_kernel<4>, dim3((unsigned)grid), block, lds, s, r); break;
+      case 5: hipLaunchKernelGGL(rs_encode8_g2_kernel<5>, dim3((unsigned)grid), block, lds, s, r); break;
+      case 6: hipLaunchKernelGGL(rs_encode8_g2_kernel<6>, dim3((unsigned)grid), block, lds, s, r); break;
+      default: hipLaunchKernelGGL(rs_encode8_g2_kernel<7>, dim3((unsigned)grid), block, lds, s, r); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
+  // General path (any k <= 128, any shard length, single codewords): LDS-resident.
   Rs8Args a;
   a.src = j.src;
   a.src_blk = j.src_blk;
@@ -414,8 +498,8 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   a.cpy_cw = j.cpy_cw;
   a.cpy_sh = j.cpy_sh;
   a.k = j.k;
-  a.log2m = ilog2(j.k);
-  a.m = 1 << a.log2m;
+  a.log2m = L;
+  a.m = 1 << L;
   a.cw_per_blk = j.cw_per_blk;
   const int units = j.shard_len / 32;  // even
   int U = 16;

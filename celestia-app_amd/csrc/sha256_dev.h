@@ -97,4 +97,50 @@ __device__ __forceinline__ void sha256_compress(uint32_t s[8], uint32_t w[16]) {
   s[7] += h;
 }
 
+// N independent compressions advanced in lockstep (round-interleaved), giving
+// the scheduler N independent dependency chains per wave.
+template <int N, int SB = 0>
+__device__ __forceinline__ void sha256_compress_n(uint32_t (&s)[N][8], uint32_t (&w)[N][16]) {
+  uint32_t a[N], b[N], c[N], d[N], e[N], f[N], g[N], h[N];
+#pragma unroll
+  for (int n = 0; n < N; n++) {
+    a[n] = s[n][0]; b[n] = s[n][1]; c[n] = s[n][2]; d[n] = s[n][3];
+    e[n] = s[n][4]; f[n] = s[n][5]; g[n] = s[n][6]; h[n] = s[n][7];
+  }
+#pragma unroll
+  for (int t = 0; t < 64; t++) {
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[n][t];
+      } else {
+        uint32_t w15 = w[n][(t - 15) & 15], w2 = w[n][(t - 2) & 15];
+        uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+        uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        wt = w[n][t & 15] + s0 + w[n][(t - 7) & 15] + s1;
+        w[n][t & 15] = wt;
+      }
+      uint32_t t1 = h[n] + xor3(rotr(e[n], 6), rotr(e[n], 11), rotr(e[n], 25)) + ch(e[n], f[n], g[n]) + K256::v[t] + wt;
+      uint32_t t2 = xor3(rotr(a[n], 2), rotr(a[n], 13), rotr(a[n], 22)) + maj(a[n], b[n], c[n]);
+      h[n] = g[n];
+      g[n] = f[n];
+      f[n] = e[n];
+      e[n] = d[n] + t1;
+      d[n] = c[n];
+      c[n] = b[n];
+      b[n] = a[n];
+      a[n] = t1 + t2;
+    }
+    // Optional scheduling fence every SB rounds: keeps the machine scheduler
+    // from hoisting message-schedule words far ahead (register pressure).
+    if (SB > 0 && (t % SB) == SB - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int n = 0; n < N; n++) {
+    s[n][0] += a[n]; s[n][1] += b[n]; s[n][2] += c[n]; s[n][3] += d[n];
+    s[n][4] += e[n]; s[n][5] += f[n]; s[n][6] += g[n]; s[n][7] += h[n];
+  }
+}
+
 }  // namespace cda

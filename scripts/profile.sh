@@ -20,6 +20,6 @@ timeout -k 5 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 step trace 300 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH
 step pmc_fetch 300 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $BENCH
 step pmc_write 300 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 $BENCH
-step pmc_valu 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_valu" -o run -- python3 $BENCH
-step pmc_lds 300 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_SALU --kernel-trace --output-format csv -d "$OUT/pmc_lds" -o run -- python3 $BENCH
+step pmc_valu 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_valu" -o run -- python3 $BENCH
+step pmc_lds 300 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM --kernel-trace --output-format csv -d "$OUT/pmc_lds" -o run -- python3 $BENCH
 find "$OUT" -name "*.csv" | head -50
