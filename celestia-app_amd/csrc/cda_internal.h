@@ -43,6 +43,7 @@ struct RsJob {
 
 // launchers (return 0 on success, -1 on launch error)
 int rs_init_device_tables(int device);
+int rs16_init_device_tables(int device);
 int launch_rs_encode8(const RsJob& job, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,

@@ -126,6 +126,10 @@ int ilog2i(uint32_t v) {
 }
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
+// Largest ODS width on the device block path: FF16 codewords up to m = 2048 in
+// LDS, DAH tree of 4k roots in one workgroup's LDS (k <= 512).
+constexpr uint32_t kMaxDeviceK = 512;
+
 void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block) {
   if (!e) return;
   e->code = code;
@@ -159,8 +163,9 @@ int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t
     j.cw_per_blk = (int)k;
     j.nblk = (int)nblocks;
     j.shard_len = CDA_SHARE;
-    ProfScope ps(c, "rs_encode8_rows", s);
-    if (launch_rs_encode8(j, s)) return CDA_E_DEVICE;
+    ProfScope ps(c, 2 * k <= 256 ? "rs_encode8_rows" : "rs_encode16_rows", s);
+    const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   {
     RsJob j{};
@@ -177,8 +182,9 @@ int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t
     j.cw_per_blk = (int)w;
     j.nblk = (int)nblocks;
     j.shard_len = CDA_SHARE;
-    ProfScope ps(c, "rs_encode8_cols", s);
-    if (launch_rs_encode8(j, s)) return CDA_E_DEVICE;
+    ProfScope ps(c, 2 * k <= 256 ? "rs_encode8_cols" : "rs_encode16_cols", s);
+    const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
   {
@@ -195,7 +201,8 @@ int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t
   }
   {
     ProfScope ps(c, "dah", s);
-    if (launch_dah(d_roots, d_dah, (int)(2 * w), (int)nblocks, s)) return CDA_E_DEVICE;
+    const int lr = launch_dah(d_roots, d_dah, (int)(2 * w), (int)nblocks, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   return CDA_OK;
 }
@@ -259,7 +266,8 @@ int cda_init(int device, cda_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return CDA_E_DEVICE;
   cda_ctx* c = new cda_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || rs_init_device_tables(device)) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || rs_init_device_tables(device) ||
+      rs16_init_device_tables(device)) {
     delete c;
     return CDA_E_DEVICE;
   }
@@ -366,7 +374,8 @@ int cda_rs_decode(cda_ctx* c, uint32_t k, uint32_t shard_len, uint8_t* shards, c
 int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds, void* d_roots,
                              void* d_dah, void* d_status, void* stream) {
   if (!c || !d_ods || !d_eds || !d_roots || !d_dah || !d_status || nblocks == 0) return CDA_E_ARG;
-  if (!is_pow2(k) || k > 128) return k > 128 ? CDA_E_UNSUPPORTED : CDA_E_NOT_POW2;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   Lock l(c);
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
   return enqueue_pipeline(c, k, nblocks, (const uint8_t*)d_ods, (uint8_t*)d_eds, d_roots, d_dah,
@@ -378,7 +387,7 @@ int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !ods || !row_roots || !col_roots || !dah || nblocks == 0) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
-  if (k > 128) return CDA_E_UNSUPPORTED;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   Lock l(c);
   const uint32_t w = 2 * k;
   const size_t ods_b = (size_t)nblocks * k * k * CDA_SHARE, eds_b = (size_t)nblocks * w * w * CDA_SHARE;

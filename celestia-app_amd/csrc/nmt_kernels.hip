@@ -122,81 +122,6 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
   for (int i = 0; i < 6; i++) out[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
 }
 
-// N shares per thread, hashed in lockstep (ILP across independent messages).
-// A[n][0..16) holds the first 64 bytes of share n.
-template <int N>
-__device__ __forceinline__ void leaf_records_n(const uint4* const (&sh)[N], uint32_t (&A)[N][16], const bool (&q0)[N],
-                                               uint4* const (&out)[N]) {
-  uint32_t ns[N][8], st[N][8], m[N][16], H[N][8];
-#pragma unroll
-  for (int n = 0; n < N; n++) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) ns[n][i] = q0[n] ? A[n][i] : 0xFFFFFFFFu;
-    sha256_init(st[n]);
-    if (q0[n]) {
-      m[n][0] = be_window(0u, A[n][0], 3);
-#pragma unroll
-      for (int i = 1; i < 7; i++) m[n][i] = be_window(A[n][i - 1], A[n][i], 3);
-      m[n][7] = (be_window(A[n][6], A[n][7], 3) & 0xFFFF0000u) | (bswap(A[n][0]) >> 16);
-    } else {
-      m[n][0] = 0x00FFFFFFu;
-#pragma unroll
-      for (int i = 1; i < 7; i++) m[n][i] = 0xFFFFFFFFu;
-      m[n][7] = 0xFFFF0000u | (bswap(A[n][0]) >> 16);
-    }
-#pragma unroll
-    for (int i = 8; i < 16; i++) m[n][i] = be_window(A[n][i - 8], A[n][i - 7], 2);
-#pragma unroll
-    for (int i = 0; i < 8; i++) H[n][i] = A[n][8 + i];
-  }
-  sha256_compress_n<N>(st, m);
-#pragma unroll
-  for (int j = 1; j < 8; j++) {
-    uint32_t C[N][16];
-#pragma unroll
-    for (int n = 0; n < N; n++) load16(sh[n] + 4 * j, C[n]);
-#pragma unroll
-    for (int n = 0; n < N; n++) {
-#pragma unroll
-      for (int i = 0; i < 7; i++) m[n][i] = be_window(H[n][i], H[n][i + 1], 2);
-      m[n][7] = be_window(H[n][7], C[n][0], 2);
-#pragma unroll
-      for (int i = 8; i < 16; i++) m[n][i] = be_window(C[n][i - 8], C[n][i - 7], 2);
-#pragma unroll
-      for (int i = 0; i < 8; i++) H[n][i] = C[n][8 + i];
-    }
-    sha256_compress_n<N>(st, m);
-  }
-#pragma unroll
-  for (int n = 0; n < N; n++) {
-#pragma unroll
-    for (int i = 0; i < 7; i++) m[n][i] = be_window(H[n][i], H[n][i + 1], 2);
-    m[n][7] = be_window(H[n][7], 0x80u, 2);
-#pragma unroll
-    for (int i = 8; i < 15; i++) m[n][i] = 0;
-    m[n][15] = 542u * 8u;
-  }
-  sha256_compress_n<N>(st, m);
-#pragma unroll
-  for (int n = 0; n < N; n++) {
-    uint32_t d[8], o[24];
-#pragma unroll
-    for (int i = 0; i < 8; i++) d[i] = bswap(st[n][i]);
-#pragma unroll
-    for (int i = 0; i < 7; i++) o[i] = ns[n][i];
-    o[7] = (ns[n][7] & 0xFFu) | (ns[n][0] << 8);
-#pragma unroll
-    for (int i = 8; i < 14; i++) o[i] = le_window(ns[n][i - 8], ns[n][i - 7], 3);
-    o[14] = (le_window(ns[n][6], ns[n][7], 3) & 0xFFFFu) | (d[0] << 16);
-#pragma unroll
-    for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
-    o[22] = d[7] >> 16;
-    o[23] = 0;
-#pragma unroll
-    for (int i = 0; i < 6; i++) out[n][i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
-  }
-}
-
 __device__ __forceinline__ void order_check_cell(const uint8_t* __restrict__ eds, const uint32_t* ns, size_t gid,
                                                  int r, int c, int k, int w, uint32_t blk,
                                                  unsigned long long* __restrict__ status) {
@@ -218,34 +143,6 @@ __device__ __forceinline__ void order_check_cell(const uint8_t* __restrict__ eds
     if (ns_cmp(nb, ns) < 0)
       atomicMin(status + blk, ((unsigned long long)CDA_AXIS_COL << 40) | ((unsigned long long)c << 20) | (r + 1));
   }
-}
-
-// N cells per thread: wave-chunks of 64*N consecutive cells, lane handles cells base+lane+64*n.
-template <int N>
-__global__ void __launch_bounds__(256) leaf_hash_kernel_n(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
-                                                          unsigned long long* __restrict__ status, int k, int log2w,
-                                                          uint32_t total_cells) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t base = wv * 64 * N + lane;
-  if (base >= total_cells) return;  // total_cells is a multiple of 64*N (checked by the launcher)
-  const int w = 1 << log2w;
-  const uint4* sh[N];
-  uint4* out[N];
-  uint32_t A[N][16];
-  bool q0[N];
-#pragma unroll
-  for (int n = 0; n < N; n++) {
-    const uint32_t gid = base + 64 * n;
-    const uint32_t cell = gid & ((1u << (2 * log2w)) - 1);
-    const int r = (int)(cell >> log2w), c = (int)(cell & (w - 1));
-    q0[n] = (r < k) && (c < k);
-    sh[n] = reinterpret_cast<const uint4*>(eds + (size_t)gid * CDA_SHARE);
-    out[n] = nodes + (size_t)gid * 6;
-    load16(sh[n], A[n]);
-    if (q0[n]) order_check_cell(eds, A[n], gid, r, c, k, w, gid >> (2 * log2w), status);
-  }
-  leaf_records_n<N>(sh, A, q0, out);
 }
 
 __global__ void __launch_bounds__(256) leaf_hash_kernel(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
@@ -525,23 +422,9 @@ int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long lon
   int log2w = 0;
   while ((1 << log2w) < w) log2w++;
   const uint32_t total = (uint32_t)nblocks * (uint32_t)w * (uint32_t)w;
-  static const int variant = [] {
-    const char* v = getenv("CDA_LEAF_VARIANT");
-    return v ? atoi(v) : 1;
-  }();
-  if (variant == 2 && total % 128 == 0) {
-    const uint32_t grid = (total / 2 + 255) / 256;
-    hipLaunchKernelGGL(leaf_hash_kernel_n<2>, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k,
-                       log2w, total);
-  } else if (variant == 3 && total % 192 == 0) {
-    const uint32_t grid = (total / 3 + 255) / 256;
-    hipLaunchKernelGGL(leaf_hash_kernel_n<3>, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k,
-                       log2w, total);
-  } else {
-    const uint32_t grid = (total + 255) / 256;
-    hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k, log2w,
-                       total);
-  }
+  const uint32_t grid = (total + 255) / 256;
+  hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k, log2w,
+                     total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "cda_internal.h"
 
 namespace cda {
@@ -514,10 +516,259 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ===========================================================================
+// GF(2^16) encoder (klauspost leopardFF16 as selected for 2k > 256).
+// Element t of every 64-byte block = byte[t] | byte[t+32] << 8; a lane's unit is
+// one 64-byte block = 32 elements = 16 bit-planes (lo bytes -> planes 0..7, hi
+// bytes -> planes 8..15).  State for one codeword x U units lives in LDS
+// ([m][16][U] words); radix-2 layers as in the FF8 path.  Multiplication in the
+// standard basis of GF(2)[x]/(x^16+x^5+x^3+x^2+1) (phi16 below), constant per
+// lane: masks from the constant's bits, or wave-uniform branches when all lanes
+// of the wave share the butterfly group (D*U >= 64).
+// ===========================================================================
+constexpr uint16_t kPhi16[16] = {0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+                                 0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E};
+constexpr uint16_t kPhiInv16[16] = {0x0001, 0x4690, 0x65D8, 0x62D0, 0x5734, 0x45F0, 0x53B8, 0x1E38,
+                                    0x7CAE, 0x4E38, 0x6708, 0xC25C, 0x7A64, 0x9EAC, 0x1124, 0x523A};
+
+__device__ __forceinline__ void apply16(uint32_t (&v)[16], const uint16_t (&cols)[16]) {
+  uint32_t o[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if ((cols[j] >> i) & 1) acc ^= v[j];
+    o[i] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) v[i] = o[i];
+}
+
+__device__ __forceinline__ void xtime16(uint32_t (&T)[16]) {  // T *= x; x^16 = x^5 + x^3 + x^2 + 1
+  const uint32_t t = T[15];
+#pragma unroll
+  for (int i = 15; i > 0; i--) T[i] = T[i - 1];
+  T[0] = t;
+  T[2] ^= t;
+  T[3] ^= t;
+  T[5] ^= t;
+}
+
+// X ^= c*Y, c wave-uniform (branches on its bits)
+__device__ __forceinline__ void gf16_muladd_uniform(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
+  uint32_t T[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) T[j] = Y[j];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if (c & (1u << i)) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) X[j] ^= T[j];
+    }
+    if (i < 15) xtime16(T);
+  }
+}
+
+// X ^= c*Y, c per lane (masks)
+__device__ __forceinline__ void gf16_muladd_lane(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
+  uint32_t T[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) T[j] = Y[j];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t mk = 0u - ((c >> i) & 1u);
+#pragma unroll
+    for (int j = 0; j < 16; j++) X[j] = __builtin_amdgcn_bitop3_b32(X[j], T[j], mk, 0x78);
+    if (i < 15) xtime16(T);
+  }
+}
+
+template <bool INVERSE, bool UNIFORM>
+__device__ __forceinline__ void butterfly16(uint32_t* st, int U, int x, int y, int u, unsigned c) {
+  uint32_t X[16], Y[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    X[j] = st[(x * 16 + j) * U + u];
+    Y[j] = st[(y * 16 + j) * U + u];
+  }
+  if (INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) Y[j] ^= X[j];
+  }
+  if (UNIFORM) {
+    if (c != 0u) gf16_muladd_uniform(X, Y, c);
+  } else {
+    gf16_muladd_lane(X, Y, c);
+  }
+  if (!INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) Y[j] ^= X[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    st[(x * 16 + j) * U + u] = X[j];
+    st[(y * 16 + j) * U + u] = Y[j];
+  }
+}
+
+struct Rs16Args {
+  const uint8_t* src;
+  long long src_blk, src_cw, src_sh;
+  uint8_t* dst;
+  long long dst_blk, dst_cw, dst_sh;
+  uint8_t* cpy;
+  long long cpy_blk, cpy_cw, cpy_sh;
+  const uint16_t* cpoly;  // [65536] per skew index: alpha^skew in std basis (0 = no multiply)
+  int k, m, log2m, cw_per_blk, U, log2U, slices;
+};
+
+template <bool INVERSE>
+__device__ __forceinline__ void rs_layer16(uint32_t* st, const Rs16Args& a, int D, int log2D) {
+  const int U = a.U;
+  const int nbu = (a.m >> 1) << a.log2U;
+  for (int bu = threadIdx.x; bu < nbu; bu += blockDim.x) {
+    const int p = bu >> a.log2U, u = bu & (U - 1);
+    const int s0 = (p >> log2D) << (log2D + 1);
+    const int x = s0 | (p & (D - 1));
+    const int y = x + D;
+    const int idx = INVERSE ? (a.m - 1 + s0 + D) : (s0 + D - 1);
+    if ((D << a.log2U) >= 64) {
+      const int sidx = __builtin_amdgcn_readfirstlane(idx);
+      butterfly16<INVERSE, true>(st, U, x, y, u, a.cpoly[sidx]);
+    } else {
+      butterfly16<INVERSE, false>(st, U, x, y, u, a.cpoly[idx]);
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) rs_encode16_kernel(Rs16Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t st[];  // [m][16][U]
+  const int U = a.U;
+  int wg = blockIdx.x;
+  const int slice = wg % a.slices;
+  wg /= a.slices;
+  const int cw = wg % a.cw_per_blk;
+  const int blk = wg / a.cw_per_blk;
+  const long long byte_off = (long long)slice * U * 64;
+  const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + byte_off;
+  uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + byte_off;
+  uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + byte_off : nullptr;
+  for (int e = threadIdx.x; e < (a.m << a.log2U); e += blockDim.x) {
+    const int s = e >> a.log2U, u = e & (U - 1);
+    uint32_t v[16];
+    if (s < a.k) {
+      const uint4* p = reinterpret_cast<const uint4*>(src + (long long)s * a.src_sh + u * 64);
+      uint4 q[4] = {p[0], p[1], p[2], p[3]};
+      if (cpy) {
+        uint4* o = reinterpret_cast<uint4*>(cpy + (long long)s * a.cpy_sh + u * 64);
+#pragma unroll
+        for (int i = 0; i < 4; i++) o[i] = q[i];
+      }
+      uint32_t lo[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
+      uint32_t hi[8] = {q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+      bitslice8(lo);
+      bitslice8(hi);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        v[j] = lo[j];
+        v[8 + j] = hi[j];
+      }
+      apply16(v, kPhi16);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) st[(s * 16 + j) * U + u] = v[j];
+  }
+  __syncthreads();
+  for (int lD = 0; lD < a.log2m; lD++) rs_layer16<true>(st, a, 1 << lD, lD);
+  for (int lD = a.log2m - 1; lD >= 0; lD--) rs_layer16<false>(st, a, 1 << lD, lD);
+  for (int e = threadIdx.x; e < (a.k << a.log2U); e += blockDim.x) {
+    const int s = e >> a.log2U, u = e & (U - 1);
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = st[(s * 16 + j) * U + u];
+    apply16(v, kPhiInv16);
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      lo[j] = v[j];
+      hi[j] = v[8 + j];
+    }
+    bitslice8(lo);
+    bitslice8(hi);
+    uint4* o = reinterpret_cast<uint4*>(dst + (long long)s * a.dst_sh + u * 64);
+    o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
+    o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+  }
+}
+
+static uint16_t* g_cpoly16[64] = {nullptr};
+
+int rs16_init_device_tables(int device) {
+  if (device < 0 || device >= 64) return -1;
+  if (g_cpoly16[device]) return 0;
+  const LeoTables& t = leo_tables(16);
+  std::vector<uint16_t> apow(65535), cpoly(65536);
+  unsigned st = 1;
+  for (int i = 0; i < 65535; i++) {
+    apow[i] = (uint16_t)st;
+    st <<= 1;
+    if (st & 0x10000) st ^= 0x1002D;
+  }
+  for (int i = 0; i < 65535; i++) cpoly[i] = t.skew[i] >= 65535 ? 0 : apow[t.skew[i]];
+  cpoly[65535] = 0;
+  void* d = nullptr;
+  if (hipMalloc(&d, 65536 * 2) != hipSuccess) return -1;
+  if (hipMemcpy(d, cpoly.data(), 65536 * 2, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (hipFuncSetAttribute((const void*)rs_encode16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
+      hipSuccess)
+    return -1;
+  g_cpoly16[device] = (uint16_t*)d;
+  return 0;
+}
+
 int launch_rs_encode16(const RsJob& j, hipStream_t s) {
-  (void)j;
-  (void)s;
-  return -2;  // GF(2^16) path: not yet on device
+  if (j.k < 1 || j.k > 32768 || j.shard_len % 64 != 0) return -2;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64 || !g_cpoly16[dev]) return -1;
+  Rs16Args a;
+  a.src = j.src;
+  a.src_blk = j.src_blk;
+  a.src_cw = j.src_cw;
+  a.src_sh = j.src_sh;
+  a.dst = j.dst;
+  a.dst_blk = j.dst_blk;
+  a.dst_cw = j.dst_cw;
+  a.dst_sh = j.dst_sh;
+  a.cpy = j.cpy;
+  a.cpy_blk = j.cpy_blk;
+  a.cpy_cw = j.cpy_cw;
+  a.cpy_sh = j.cpy_sh;
+  a.cpoly = g_cpoly16[dev];
+  a.k = j.k;
+  a.log2m = ilog2(j.k);
+  a.m = 1 << a.log2m;
+  a.cw_per_blk = j.cw_per_blk;
+  const int units = j.shard_len / 64;
+  // LDS budget 128 KiB: m * 64 B per unit column
+  int U = 8;
+  while (U > 1 && ((size_t)a.m * 64 * U > 64 * 1024 || units % U)) U >>= 1;
+  if ((size_t)a.m * 64 * U > 128 * 1024) return -2;  // m > 2048: not on the device path yet
+  a.U = U;
+  a.log2U = ilog2(U);
+  a.slices = units / U;
+  const size_t lds = (size_t)a.m * 16 * U * 4;
+  const long long grid = (long long)j.nblk * j.cw_per_blk * a.slices;
+  if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
+  hipLaunchKernelGGL(rs_encode16_kernel, dim3((unsigned)grid), dim3(256), lds, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace cda

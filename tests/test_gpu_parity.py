@@ -42,7 +42,7 @@ def test_extend_shares_errors(ctx, count):
 
 
 # ---- seeded random squares vs the oracle ---------------------------------------------------
-@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128])
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128, 256, 512])
 def test_extend_commit_matches_oracle(ctx, k):
     ods = O.gen_ods(k, 0xC0FFEE + k)
     rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods)
@@ -95,6 +95,15 @@ def test_column_order_violation(ctx):
 @pytest.mark.parametrize("L", [64, 512, 1024])
 def test_rs_encode_matches_oracle(ctx, k, L):
     rng = np.random.default_rng(k * 1000 + L)
+    d = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    assert np.array_equal(ctx.rs_encode(d), O.leo_encode(d))
+
+
+@pytest.mark.parametrize("k", [129, 200, 256, 300, 512, 1000, 1024, 2048])
+@pytest.mark.parametrize("L", [64, 512])
+def test_rs_encode_ff16_matches_oracle(ctx, k, L):
+    """GF(2^16) Leopard (2k > 256): lo/hi byte element layout per 64-byte block."""
+    rng = np.random.default_rng(k * 7 + L)
     d = rng.integers(0, 256, (k, L), dtype=np.uint8)
     assert np.array_equal(ctx.rs_encode(d), O.leo_encode(d))
 
