@@ -44,6 +44,12 @@ struct RsJob {
 // launchers (return 0 on success, -1 on launch error)
 int rs_init_device_tables(int device);
 int rs16_init_device_tables(int device);
+int rs_decode_init_device_tables(int device);
+// Batched erasure decode of ncw codewords of 2k shards each (data then parity);
+// shard i of codeword c at d_base + d_off[c] + i * d_stride[c]; present[c][2k].
+// Missing shards are written in place.
+int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d_stride, const uint8_t* d_present,
+                     int ncw, int k, int shard_len, hipStream_t s);
 int launch_rs_encode8(const RsJob& job, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,

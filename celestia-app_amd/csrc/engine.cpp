@@ -266,8 +266,13 @@ int cda_init(int device, cda_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return CDA_E_DEVICE;
   cda_ctx* c = new cda_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || rs_init_device_tables(device) ||
-      rs16_init_device_tables(device)) {
+  const char* fail = nullptr;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) fail = "stream";
+  else if (rs_init_device_tables(device)) fail = "rs8 tables";
+  else if (rs16_init_device_tables(device)) fail = "rs16 tables";
+  else if (rs_decode_init_device_tables(device)) fail = "decode tables";
+  if (fail) {
+    fprintf(stderr, "cda_init: %s initialisation failed: %s\n", fail, hipGetErrorString(hipGetLastError()));
     delete c;
     return CDA_E_DEVICE;
   }
@@ -368,7 +373,32 @@ int cda_rs_decode(cda_ctx* c, uint32_t k, uint32_t shard_len, uint8_t* shards, c
   for (uint32_t i = 0; i < 2 * k; i++) np += present[i] ? 1 : 0;
   if (np < k) return CDA_E_TOO_FEW;
   if (np == 2 * k) return CDA_OK;
-  return CDA_E_UNSUPPORTED;
+  Lock l(c);
+  const size_t bytes = (size_t)2 * k * shard_len;
+  int rc;
+  if ((rc = ensure(c, c->eds, bytes)) || (rc = ensure(c, c->ods, 64 + 2 * (size_t)k))) return rc;
+  // descriptor block: off[1], stride[1], present[2k]
+  std::vector<uint8_t> desc(16 + 2 * (size_t)k);
+  const long long off = 0, stride = shard_len;
+  memcpy(desc.data(), &off, 8);
+  memcpy(desc.data() + 8, &stride, 8);
+  for (uint32_t i = 0; i < 2 * k; i++) desc[16 + i] = present[i] ? 1 : 0;
+  hipStream_t s = c->stream;
+  if (!dev_ok(c, hipMemcpyAsync(c->eds.p, shards, bytes, hipMemcpyHostToDevice, s), "H2D") ||
+      !dev_ok(c, hipMemcpyAsync(c->ods.p, desc.data(), desc.size(), hipMemcpyHostToDevice, s), "H2D"))
+    return CDA_E_DEVICE;
+  {
+    ProfScope ps(c, "rs_decode", s);
+    const uint8_t* d = (const uint8_t*)c->ods.p;
+    const int lr = launch_rs_decode((uint8_t*)c->eds.p, (const long long*)d, (const long long*)(d + 8), d + 16, 1,
+                                    (int)k, (int)shard_len, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+  }
+  if (!dev_ok(c, hipMemcpyAsync(shards, c->eds.p, bytes, hipMemcpyDeviceToHost, s), "D2H") ||
+      !dev_ok(c, hipStreamSynchronize(s), "sync"))
+    return CDA_E_DEVICE;
+  flush_profile(c);
+  return CDA_OK;
 }
 
 int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds, void* d_roots,

@@ -1,0 +1,424 @@
+// rs_decode.hip — Leopard erasure decoding on gfx950 (rsmt2d LeoRSCodec.Decode
+// -> klauspost/reedsolomon v1.12.1 leopardFF8/FF16 reconstruct; upstream,
+// pinned go.mod:153).  Used by cda_rs_decode and by the Repair driver.
+//
+// Per codeword (k data, k parity, m = ceilPow2(k), n = 2m), as in the reference:
+//   E = erased positions of the n-space: parity i missing -> i, i in [k, m) -> i,
+//       data i missing -> m + i
+//   errLocs[p] = sum_{j in E, j != p} log(p ^ j)   (mod 2^bits - 1)
+//     (the reference gets the same values via two Walsh-Hadamard transforms)
+//   work[p] = shard(p) * exp(errLocs[p]) for present p, 0 otherwise
+//   work = FFT_DIT( FormalDerivative( IFFT_DIT(work) ) )   (skew[s + D - 1], size n)
+//   missing shard(p) = work[p] * exp(-errLocs[p])
+// FormalDerivative: new[x] = old[x] ^ XOR_{b: bit b of x is 0} old[x + 2^b]
+// (closed form of the reference's "work[i-w..i) ^= work[i..i+w)" loop).
+// The code is MDS, so the output equals any other correct decoder's; the tests
+// compare it with the oracle's Lagrange decoder.
+//
+// Layout: one workgroup per (codeword, unit slice); state [n][PL planes][U] in LDS,
+// bit-sliced and in the standard polynomial basis (see rs_kernels.hip).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "cda_internal.h"
+
+namespace cda {
+namespace dec {
+
+__device__ __forceinline__ void swapmove(uint32_t& a, uint32_t& b, uint32_t mask, int n) {
+  uint32_t t = __builtin_amdgcn_bitop3_b32(a >> n, b, mask, 0x28);
+  b ^= t;
+  a ^= t << n;
+}
+__device__ __forceinline__ void bitslice8(uint32_t* w) {
+  swapmove(w[0], w[1], 0x55555555u, 1);
+  swapmove(w[2], w[3], 0x55555555u, 1);
+  swapmove(w[4], w[5], 0x55555555u, 1);
+  swapmove(w[6], w[7], 0x55555555u, 1);
+  swapmove(w[0], w[2], 0x33333333u, 2);
+  swapmove(w[1], w[3], 0x33333333u, 2);
+  swapmove(w[4], w[6], 0x33333333u, 2);
+  swapmove(w[5], w[7], 0x33333333u, 2);
+  swapmove(w[0], w[4], 0x0F0F0F0Fu, 4);
+  swapmove(w[1], w[5], 0x0F0F0F0Fu, 4);
+  swapmove(w[2], w[6], 0x0F0F0F0Fu, 4);
+  swapmove(w[3], w[7], 0x0F0F0F0Fu, 4);
+}
+
+template <int PL>
+struct Field;
+template <>
+struct Field<8> {
+  static constexpr unsigned kMod = 255;
+  static constexpr uint16_t phi[8] = {1, 214, 152, 146, 86, 200, 88, 230};
+  static constexpr uint16_t phi_inv[8] = {1, 104, 92, 100, 114, 240, 86, 18};
+  __device__ static void xtime(uint32_t (&T)[8]) {  // x^8 = x^4+x^3+x^2+1
+    const uint32_t t = T[7];
+#pragma unroll
+    for (int i = 7; i > 0; i--) T[i] = T[i - 1];
+    T[0] = t;
+    T[2] ^= t;
+    T[3] ^= t;
+    T[4] ^= t;
+  }
+};
+template <>
+struct Field<16> {
+  static constexpr unsigned kMod = 65535;
+  static constexpr uint16_t phi[16] = {0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+                                       0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E};
+  static constexpr uint16_t phi_inv[16] = {0x0001, 0x4690, 0x65D8, 0x62D0, 0x5734, 0x45F0, 0x53B8, 0x1E38,
+                                           0x7CAE, 0x4E38, 0x6708, 0xC25C, 0x7A64, 0x9EAC, 0x1124, 0x523A};
+  __device__ static void xtime(uint32_t (&T)[16]) {  // x^16 = x^5+x^3+x^2+1
+    const uint32_t t = T[15];
+#pragma unroll
+    for (int i = 15; i > 0; i--) T[i] = T[i - 1];
+    T[0] = t;
+    T[2] ^= t;
+    T[3] ^= t;
+    T[5] ^= t;
+  }
+};
+
+template <int PL>
+__device__ __forceinline__ void apply(uint32_t (&v)[PL], const uint16_t (&cols)[PL]) {
+  uint32_t o[PL];
+#pragma unroll
+  for (int i = 0; i < PL; i++) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < PL; j++)
+      if ((cols[j] >> i) & 1) acc ^= v[j];
+    o[i] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < PL; i++) v[i] = o[i];
+}
+
+// X ^= c*Y (std basis), c per lane
+template <int PL>
+__device__ __forceinline__ void muladd_lane(uint32_t (&X)[PL], const uint32_t (&Y)[PL], unsigned c) {
+  uint32_t T[PL];
+#pragma unroll
+  for (int j = 0; j < PL; j++) T[j] = Y[j];
+#pragma unroll
+  for (int i = 0; i < PL; i++) {
+    const uint32_t mk = 0u - ((c >> i) & 1u);
+#pragma unroll
+    for (int j = 0; j < PL; j++) X[j] = __builtin_amdgcn_bitop3_b32(X[j], T[j], mk, 0x78);
+    if (i < PL - 1) Field<PL>::xtime(T);
+  }
+}
+// X = c*Y
+template <int PL>
+__device__ __forceinline__ void mul_lane(uint32_t (&X)[PL], const uint32_t (&Y)[PL], unsigned c) {
+#pragma unroll
+  for (int j = 0; j < PL; j++) X[j] = 0;
+  muladd_lane<PL>(X, Y, c);
+}
+
+// raw bytes (unit) <-> planes
+template <int PL>
+__device__ __forceinline__ void load_unit(const uint8_t* p, uint32_t (&v)[PL]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  if (PL == 8) {
+    const uint4 a = q[0], b = q[1];
+    uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bitslice8(w);
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = w[j];
+  } else {
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    uint32_t lo[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t hi[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    bitslice8(lo);
+    bitslice8(hi);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      v[j] = lo[j];
+      v[(8 + j) % PL] = hi[j];
+    }
+  }
+  apply<PL>(v, Field<PL>::phi);
+}
+template <int PL>
+__device__ __forceinline__ void store_unit(uint8_t* p, uint32_t (&v)[PL]) {
+  apply<PL>(v, Field<PL>::phi_inv);
+  uint4* q = reinterpret_cast<uint4*>(p);
+  if (PL == 8) {
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = v[j];
+    bitslice8(w);
+    q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      lo[j] = v[j];
+      hi[j] = v[(8 + j) % PL];
+    }
+    bitslice8(lo);
+    bitslice8(hi);
+    q[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    q[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
+    q[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    q[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+  }
+}
+
+struct DecArgs {
+  uint8_t* base;                // shard i of codeword c at base + off[c] + i * stride[c] (+ slice/unit offset)
+  const long long* off;         // [ncw]
+  const long long* stride;      // [ncw]
+  const uint8_t* present;       // [ncw][2k]
+  const uint16_t* log_t;        // field log table (Leopard representation)
+  const uint16_t* apow;         // alpha^i in the standard basis, i in [0, mod)
+  const uint16_t* skew;         // FFT skew table (log values)
+  int k, m, log2m, n, log2n, U, log2U, slices;
+};
+
+template <int PL>
+__device__ __forceinline__ unsigned cpoly_of_log(const DecArgs& a, unsigned l) {
+  return a.apow[l % Field<PL>::kMod];
+}
+
+template <int PL, bool INVERSE>
+__device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int log2D) {
+  const int U = a.U;
+  const int nbu = (a.n >> 1) << a.log2U;
+  for (int bu = threadIdx.x; bu < nbu; bu += blockDim.x) {
+    const int p = bu >> a.log2U, u = bu & (U - 1);
+    const int s0 = (p >> log2D) << (log2D + 1);
+    const int x = s0 | (p & (D - 1));
+    const int y = x + D;
+    const unsigned lm = a.skew[s0 + D - 1];
+    uint32_t X[PL], Y[PL];
+#pragma unroll
+    for (int j = 0; j < PL; j++) {
+      X[j] = st[(x * PL + j) * U + u];
+      Y[j] = st[(y * PL + j) * U + u];
+    }
+    if (INVERSE) {
+#pragma unroll
+      for (int j = 0; j < PL; j++) Y[j] ^= X[j];
+      if (lm != Field<PL>::kMod) muladd_lane<PL>(X, Y, a.apow[lm]);
+    } else {
+      if (lm != Field<PL>::kMod) muladd_lane<PL>(X, Y, a.apow[lm]);
+#pragma unroll
+      for (int j = 0; j < PL; j++) Y[j] ^= X[j];
+    }
+#pragma unroll
+    for (int j = 0; j < PL; j++) {
+      st[(x * PL + j) * U + u] = X[j];
+      st[(y * PL + j) * U + u] = Y[j];
+    }
+  }
+  __syncthreads();
+}
+
+template <int PL>
+__global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* st = smem;                                                        // [n][PL][U]
+  uint16_t* errl = reinterpret_cast<uint16_t*>(smem + (size_t)a.n * PL * a.U);  // [n]
+  uint16_t* elist = errl + a.n;                                                // [n]
+  __shared__ int ecount;
+  const int U = a.U;
+  int wg = blockIdx.x;
+  const int slice = wg % a.slices;
+  const int cw = wg / a.slices;
+  const uint8_t* pres = a.present + (size_t)cw * 2 * a.k;
+  uint8_t* base = a.base + a.off[cw] + (long long)slice * U * (PL * 4);
+  const long long sstride = a.stride[cw];
+
+  // erasure set in n-space
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int i = 0; i < a.m; i++)
+      if (i >= a.k || !pres[a.k + i]) elist[c++] = (uint16_t)i;
+    for (int i = 0; i < a.k; i++)
+      if (!pres[i]) elist[c++] = (uint16_t)(a.m + i);
+    ecount = c;
+  }
+  __syncthreads();
+  const int ne = ecount;
+  for (int p = threadIdx.x; p < a.m + a.k; p += blockDim.x) {
+    unsigned long long acc = 0;
+    for (int t = 0; t < ne; t++) {
+      const int j = elist[t];
+      if (j != p) acc += a.log_t[p ^ j];
+    }
+    errl[p] = (uint16_t)(acc % Field<PL>::kMod);
+  }
+  __syncthreads();
+  // work[p] = shard(p) * exp(errLocs[p]) (present), else 0
+  for (int e = threadIdx.x; e < (a.n << a.log2U); e += blockDim.x) {
+    const int p = e >> a.log2U, u = e & (U - 1);
+    int shard = -1;
+    if (p < a.k) shard = pres[a.k + p] ? a.k + p : -1;
+    else if (p >= a.m && p < a.m + a.k) shard = pres[p - a.m] ? p - a.m : -1;
+    uint32_t v[PL];
+    if (shard >= 0) {
+      uint32_t raw[PL];
+      load_unit<PL>(base + shard * sstride + u * (PL * 4), raw);
+      mul_lane<PL>(v, raw, cpoly_of_log<PL>(a, errl[p]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < PL; j++) v[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < PL; j++) st[(p * PL + j) * U + u] = v[j];
+  }
+  __syncthreads();
+  for (int lD = 0; lD < a.log2n; lD++) layer<PL, true>(st, a, 1 << lD, lD);
+  // formal derivative (out of place through registers; <= 4 items per thread)
+  {
+    uint32_t nv[4][PL];
+    const int items = a.n << a.log2U;
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+      const int e = threadIdx.x + it * blockDim.x;
+      if (e < items) {
+        const int x = e >> a.log2U, u = e & (U - 1);
+#pragma unroll
+        for (int j = 0; j < PL; j++) nv[it][j] = st[(x * PL + j) * U + u];
+        for (int b = 0; b < a.log2n; b++) {
+          if ((x >> b) & 1) continue;
+          const int y = x + (1 << b);
+#pragma unroll
+          for (int j = 0; j < PL; j++) nv[it][j] ^= st[(y * PL + j) * U + u];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+      const int e = threadIdx.x + it * blockDim.x;
+      if (e < items) {
+        const int x = e >> a.log2U, u = e & (U - 1);
+#pragma unroll
+        for (int j = 0; j < PL; j++) st[(x * PL + j) * U + u] = nv[it][j];
+      }
+    }
+    __syncthreads();
+  }
+  for (int lD = a.log2n - 1; lD >= 0; lD--) layer<PL, false>(st, a, 1 << lD, lD);
+  // reveal erasures: missing shard(p) = work[p] * exp(-errLocs[p])
+  for (int e = threadIdx.x; e < (a.n << a.log2U); e += blockDim.x) {
+    const int p = e >> a.log2U, u = e & (U - 1);
+    int shard = -1;
+    if (p < a.k) shard = pres[a.k + p] ? -1 : a.k + p;
+    else if (p >= a.m && p < a.m + a.k) shard = pres[p - a.m] ? -1 : p - a.m;
+    if (shard < 0) continue;
+    uint32_t w[PL], v[PL];
+#pragma unroll
+    for (int j = 0; j < PL; j++) w[j] = st[(p * PL + j) * U + u];
+    const unsigned l = (Field<PL>::kMod - errl[p]) % Field<PL>::kMod;
+    mul_lane<PL>(v, w, cpoly_of_log<PL>(a, l));
+    store_unit<PL>(base + shard * sstride + u * (PL * 4), v);
+  }
+}
+
+struct Tables {
+  uint16_t* log_t = nullptr;
+  uint16_t* apow = nullptr;
+  uint16_t* skew = nullptr;
+};
+static Tables g_tab[2][64];
+
+static int upload(int device, int bits) {
+  Tables& t = g_tab[bits == 16][device];
+  if (t.log_t) return 0;
+  const LeoTables& lt = leo_tables(bits);
+  const unsigned order = lt.order, mod = lt.modulus;
+  const unsigned poly = bits == 8 ? 0x11D : 0x1002D;
+  std::vector<uint16_t> apow(order, 0), skew(order, (uint16_t)mod);
+  unsigned s = 1;
+  for (unsigned i = 0; i < mod; i++) {
+    apow[i] = (uint16_t)s;
+    s <<= 1;
+    if (s & order) s ^= poly;
+  }
+  for (unsigned i = 0; i < mod; i++) skew[i] = lt.skew[i];
+  void *a = nullptr, *b = nullptr, *c = nullptr;
+  if (hipMalloc(&a, order * 2) != hipSuccess || hipMalloc(&b, order * 2) != hipSuccess ||
+      hipMalloc(&c, order * 2) != hipSuccess)
+    return -1;
+  if (hipMemcpy(a, lt.log_t, order * 2, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(b, apow.data(), order * 2, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c, skew.data(), order * 2, hipMemcpyHostToDevice) != hipSuccess)
+    return -1;
+  t.log_t = (uint16_t*)a;
+  t.apow = (uint16_t*)b;
+  t.skew = (uint16_t*)c;
+  return 0;
+}
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) l++;
+  return l;
+}
+
+}  // namespace dec
+
+constexpr int kDecMaxLds = 144 * 1024;
+
+int rs_decode_init_device_tables(int device) {
+  if (device < 0 || device >= 64) return -1;
+  if (dec::upload(device, 8) || dec::upload(device, 16)) return -1;
+  if (hipFuncSetAttribute((const void*)dec::rs_decode_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kDecMaxLds) != hipSuccess ||
+      hipFuncSetAttribute((const void*)dec::rs_decode_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kDecMaxLds) != hipSuccess)
+    return -1;
+  return 0;
+}
+
+int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d_stride, const uint8_t* d_present,
+                     int ncw, int k, int shard_len, hipStream_t s) {
+  if (k < 1 || k > 32768 || shard_len % 64 != 0 || ncw <= 0) return -2;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return -1;
+  const bool ff16 = 2 * k > 256;
+  const dec::Tables& t = dec::g_tab[ff16][dev];
+  if (!t.log_t) return -1;
+  dec::DecArgs a;
+  a.base = d_base;
+  a.off = d_off;
+  a.stride = d_stride;
+  a.present = d_present;
+  a.log_t = t.log_t;
+  a.apow = t.apow;
+  a.skew = t.skew;
+  a.k = k;
+  a.log2m = dec::ilog2(k);
+  a.m = 1 << a.log2m;
+  a.n = 2 * a.m;
+  a.log2n = a.log2m + 1;
+  const int PL = ff16 ? 16 : 8;
+  const int unit = PL * 4;  // bytes per lane unit
+  const int units = shard_len / unit;
+  int U = 16;
+  while (U > 1 && (units % U || a.n * U > 1024)) U >>= 1;  // <= 4 derivative items per thread
+  if (a.n * U > 1024) return -2;                          // n > 1024 (k > 512): not on the device path yet
+  a.U = U;
+  a.log2U = dec::ilog2(U);
+  a.slices = units / U;
+  const size_t lds = (size_t)a.n * PL * U * 4 + (size_t)a.n * 4;
+  if (lds > (size_t)kDecMaxLds) return -2;
+  const long long grid = (long long)ncw * a.slices;
+  if (grid > 0x7FFFFFFF) return -2;
+  if (ff16)
+    hipLaunchKernelGGL(dec::rs_decode_kernel<16>, dim3((unsigned)grid), dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL(dec::rs_decode_kernel<8>, dim3((unsigned)grid), dim3(256), lds, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cda

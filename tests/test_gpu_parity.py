@@ -155,3 +155,38 @@ def test_dah_hash_any_count(ctx, n):
     rr = rng.integers(0, 256, (n, 90), dtype=np.uint8)
     cr = rng.integers(0, 256, (n, 90), dtype=np.uint8)
     assert ctx.dah_hash(rr, cr) == O.dah_hash(rr, cr)
+
+
+# ---- decode (rsmt2d LeoRSCodec.Decode) -------------------------------------------------------
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 8, 16, 33, 64, 128, 129, 256, 300, 512])
+def test_rs_decode_matches_oracle(ctx, k):
+    rng = np.random.default_rng(1000 + k)
+    L = 512 if k <= 256 else 128
+    d = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    full = np.concatenate([d, O.leo_encode(d)])
+    for trial in range(3):
+        nkeep = k + trial * (k // 3)
+        pres = np.zeros(2 * k, np.uint8)
+        pres[rng.choice(2 * k, min(nkeep, 2 * k), replace=False)] = 1
+        damaged = np.where(pres[:, None] == 1, full, 0x5C).astype(np.uint8)
+        got = ctx.rs_decode(damaged, pres)
+        assert np.array_equal(got, full), f"trial {trial}"
+
+
+def test_rs_decode_too_few(ctx):
+    from cda import CdaError
+    k = 8
+    pres = np.zeros(16, np.uint8)
+    pres[:7] = 1
+    with pytest.raises(CdaError) as ei:
+        ctx.rs_decode(np.zeros((16, 64), np.uint8), pres)
+    assert ei.value.code == -6
+
+
+def test_codec_decode_interface(ctx):
+    from cda.rsmt2d import LeoRSCodec
+    c = LeoRSCodec(ctx)
+    data = [bytes([i * 3 + 1]) * 512 for i in range(4)]
+    full = data + c.encode(data)
+    shards = [s if i in (1, 4, 6, 7) else None for i, s in enumerate(full)]
+    assert c.decode(shards) == full
