@@ -60,6 +60,11 @@ int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks,
 int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,
                      unsigned long long* d_status, hipStream_t s);
 int launch_level_generic(const void* d_in, void* d_out, int n_in, hipStream_t s);
+// roots of ntrees EDS axes (axes[t] = axis << 24 | index), 96-B records into d_roots
+int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int ntrees, void* d_nodes, void* d_scratch,
+                      void* d_roots, unsigned long long* d_status, hipStream_t s);
+int launch_parity_compare(const uint8_t* d_eds, int k, const int* d_axes, int naxes, const uint8_t* d_par,
+                          unsigned* d_flags, hipStream_t s);
 
 // profiling hook implemented by the engine
 struct ProfScope {

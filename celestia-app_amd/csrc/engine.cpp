@@ -601,11 +601,250 @@ int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uin
   return CDA_OK;
 }
 
+// rsmt2d (*ExtendedDataSquare).Repair (v0.12.0, upstream):
+//   prerepairSanityCheck: every complete row/col must match its root and
+//     re-encode to its parity (ErrByzantineData otherwise);
+//   solveCrossword: sweeps of "row i, then col i" for i = 0..w-1; an incomplete
+//     axis with >= k shares is decoded, its root and the roots of orthogonal
+//     axes it completes are verified, then its cells are inserted; a sweep
+//     without progress is ErrUnrepairableDataSquare.
+// The host replays exactly that order on the presence bitmap (control only) and
+// runs every decode / root / re-encode on the GPU, batching consecutive
+// operations that are already decodable at the batch start.  On a Byzantine
+// failure the cells of the failing operation and of later operations in its
+// batch are marked missing again, leaving the square "most repaired prior to the
+// Byzantine axis" as the reference does.
+namespace {
+inline int enc_axis(int axis, int idx) { return (axis << 24) | idx; }
+}
+
 int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, cda_err_info* err) {
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
-  return CDA_E_UNSUPPORTED;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
+  Lock l(c);
+  const int w = (int)(2 * k), K = (int)k;
+  const size_t ncell = (size_t)w * w, eds_b = ncell * CDA_SHARE;
+  hipStream_t s = c->stream;
+  int rc;
+  // workspace: eds | parity scratch (2 * w * k shards) | roots/nodes/scratch for up to 2w trees
+  const size_t trees_cap = (size_t)2 * w;
+  if ((rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->ods, eds_b)) ||
+      (rc = ensure(c, c->leaf, trees_cap * w * CDA_REC_BYTES)) ||
+      (rc = ensure(c, c->scratch, trees_cap * w * CDA_REC_BYTES)) ||
+      (rc = ensure(c, c->roots, trees_cap * CDA_REC_BYTES)) || (rc = ensure(c, c->status, trees_cap * 8 + 64)) ||
+      (rc = ensure(c, c->dah, trees_cap * (16 + 2 * (size_t)w) + trees_cap * 4 + 64)))
+    return rc;
+  uint8_t* d_eds = (uint8_t*)c->eds.p;
+  uint8_t* d_par = (uint8_t*)c->ods.p;
+  if (!dev_ok(c, hipMemcpyAsync(d_eds, eds, eds_b, hipMemcpyHostToDevice, s), "H2D")) return CDA_E_DEVICE;
+  std::vector<uint8_t> P(present, present + ncell);
+  for (auto& v : P) v = v ? 1 : 0;
+  auto cell = [&](int axis, int idx, int i) -> size_t {
+    return axis == CDA_AXIS_ROW ? (size_t)idx * w + i : (size_t)i * w + idx;
+  };
+  auto count = [&](const std::vector<uint8_t>& p, int axis, int idx, int skip) {
+    int n = 0;
+    for (int i = 0; i < w; i++) n += (i != skip && p[cell(axis, idx, i)]) ? 1 : 0;
+    return n;
+  };
+  const uint8_t* want[2] = {row_roots, col_roots};
+  // GPU roots of a list of axes -> host records
+  std::vector<uint8_t> recs;
+  std::vector<uint64_t> st;
+  auto roots_of = [&](const std::vector<int>& axes) -> int {
+    if (axes.empty()) return CDA_OK;
+    if (axes.size() > trees_cap) return CDA_E_ARG;
+    int* d_axes = (int*)c->dah.p;
+    if (!dev_ok(c, hipMemcpyAsync(d_axes, axes.data(), axes.size() * 4, hipMemcpyHostToDevice, s), "H2D") ||
+        !dev_ok(c, hipMemsetAsync(c->status.p, 0xFF, axes.size() * 8, s), "memset"))
+      return CDA_E_DEVICE;
+    {
+      ProfScope ps(c, "repair_roots", s);
+      if (launch_axes_roots(d_eds, K, d_axes, (int)axes.size(), c->leaf.p, c->scratch.p, c->roots.p,
+                            (unsigned long long*)c->status.p, s))
+        return CDA_E_DEVICE;
+    }
+    recs.resize(axes.size() * CDA_REC_BYTES);
+    st.resize(axes.size());
+    if (!dev_ok(c, hipMemcpyAsync(recs.data(), c->roots.p, recs.size(), hipMemcpyDeviceToHost, s), "D2H") ||
+        !dev_ok(c, hipMemcpyAsync(st.data(), c->status.p, st.size() * 8, hipMemcpyDeviceToHost, s), "D2H") ||
+        !dev_ok(c, hipStreamSynchronize(s), "sync"))
+      return CDA_E_DEVICE;
+    return CDA_OK;
+  };
+  auto root_ok = [&](size_t t, int axis_code) {
+    const int axis = axis_code >> 24, idx = axis_code & 0xFFFFFF;
+    if (st[t] != ~0ull) return false;  // push error => byzantine
+    return memcmp(recs.data() + t * CDA_REC_BYTES, want[axis] + (size_t)idx * CDA_NODE_SIZE, CDA_NODE_SIZE) == 0;
+  };
+  auto finish = [&](int code, int axis, int idx) -> int {
+    if (!dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H") ||
+        !dev_ok(c, hipStreamSynchronize(s), "sync"))
+      return CDA_E_DEVICE;
+    flush_profile(c);
+    memcpy(present, P.data(), ncell);
+    if (code != CDA_OK) set_err(err, code, axis, idx, -1, -1);
+    return code;
+  };
+
+  // ---- prerepairSanityCheck ----
+  {
+    std::vector<int> axes;
+    std::vector<uint8_t> rowc(w), colc(w);
+    for (int i = 0; i < w; i++) {
+      rowc[i] = count(P, CDA_AXIS_ROW, i, -1) == w;
+      colc[i] = count(P, CDA_AXIS_COL, i, -1) == w;
+      if (rowc[i]) axes.push_back(enc_axis(CDA_AXIS_ROW, i));
+      if (colc[i]) axes.push_back(enc_axis(CDA_AXIS_COL, i));
+    }
+    std::vector<unsigned> pflag_row(w, 0), pflag_col(w, 0);
+    if (!axes.empty()) {
+      if ((rc = roots_of(axes))) return rc;
+      // re-encode every row and column data half; compare the complete ones
+      unsigned* d_flags = (unsigned*)((uint8_t*)c->dah.p + trees_cap * (16 + 2 * (size_t)w));
+      int* d_axes = (int*)c->dah.p;
+      std::vector<int> all(2 * w);
+      for (int i = 0; i < w; i++) {
+        all[i] = enc_axis(CDA_AXIS_ROW, i);
+        all[w + i] = enc_axis(CDA_AXIS_COL, i);
+      }
+      if (!dev_ok(c, hipMemcpyAsync(d_axes, all.data(), all.size() * 4, hipMemcpyHostToDevice, s), "H2D") ||
+          !dev_ok(c, hipMemsetAsync(d_flags, 0, 2 * w * 4, s), "memset"))
+        return CDA_E_DEVICE;
+      for (int axis = 0; axis < 2; axis++) {
+        RsJob j{};
+        j.src = d_eds;
+        j.src_cw = axis == CDA_AXIS_ROW ? (long long)w * CDA_SHARE : CDA_SHARE;
+        j.src_sh = axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
+        j.dst = d_par + (size_t)axis * w * K * CDA_SHARE;
+        j.dst_cw = (long long)K * CDA_SHARE;
+        j.dst_sh = CDA_SHARE;
+        j.k = K;
+        j.cw_per_blk = w;
+        j.nblk = 1;
+        j.shard_len = CDA_SHARE;
+        ProfScope ps(c, "repair_reencode", s);
+        const int lr = 2 * K <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
+        if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+        if (launch_parity_compare(d_eds, K, d_axes + axis * w, w, j.dst, d_flags + axis * w, s)) return CDA_E_DEVICE;
+      }
+      std::vector<unsigned> fl(2 * w);
+      if (!dev_ok(c, hipMemcpyAsync(fl.data(), d_flags, 2 * w * 4, hipMemcpyDeviceToHost, s), "D2H") ||
+          !dev_ok(c, hipStreamSynchronize(s), "sync"))
+        return CDA_E_DEVICE;
+      for (int i = 0; i < w; i++) {
+        pflag_row[i] = fl[i];
+        pflag_col[i] = fl[w + i];
+      }
+      // report in a fixed order: i ascending; row root, col root, row parity, col parity
+      size_t t = 0;
+      std::vector<int> rok(w, 1), cok(w, 1);
+      for (int i = 0; i < w; i++) {
+        if (rowc[i]) rok[i] = root_ok(t++, enc_axis(CDA_AXIS_ROW, i));
+        if (colc[i]) cok[i] = root_ok(t++, enc_axis(CDA_AXIS_COL, i));
+      }
+      for (int i = 0; i < w; i++) {
+        if (rowc[i] && !rok[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_ROW, i);
+        if (colc[i] && !cok[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_COL, i);
+        if (rowc[i] && pflag_row[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_ROW, i);
+        if (colc[i] && pflag_col[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_COL, i);
+      }
+    }
+  }
+
+  // ---- solveCrossword ----
+  struct Op {
+    int axis, idx;
+    std::vector<int> ortho;
+  };
+  long long* d_off = (long long*)c->dah.p;
+  long long* d_stride = d_off + trees_cap;
+  uint8_t* d_pres = (uint8_t*)(d_stride + trees_cap);
+  for (;;) {
+    // replay one sweep on the presence bitmap
+    std::vector<uint8_t> Ps = P;
+    std::vector<Op> ops;
+    bool solved = true, progress = false;
+    for (int i = 0; i < w; i++) {
+      for (int axis = 0; axis < 2; axis++) {
+        const int n = count(Ps, axis, i, -1);
+        if (n == w) continue;
+        if (n < K) {
+          solved = false;
+          continue;
+        }
+        Op op{axis, i, {}};
+        for (int j = 0; j < w; j++) {
+          if (Ps[cell(axis, i, j)]) continue;
+          const int oaxis = 1 - axis;
+          if (count(Ps, oaxis, j, i) == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
+        }
+        for (int j = 0; j < w; j++) Ps[cell(axis, i, j)] = 1;
+        ops.push_back(std::move(op));
+        progress = true;
+      }
+    }
+    // execute in batches of operations already decodable at the batch start
+    size_t b0 = 0;
+    while (b0 < ops.size()) {
+      size_t b1 = b0;
+      while (b1 < ops.size() && b1 - b0 < trees_cap / 2 && count(P, ops[b1].axis, ops[b1].idx, -1) >= K) b1++;
+      if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
+      const int nb = (int)(b1 - b0);
+      std::vector<long long> off(nb), stride(nb);
+      std::vector<uint8_t> pres((size_t)nb * w);
+      for (int q = 0; q < nb; q++) {
+        const Op& op = ops[b0 + q];
+        off[q] = op.axis == CDA_AXIS_ROW ? (long long)op.idx * w * CDA_SHARE : (long long)op.idx * CDA_SHARE;
+        stride[q] = op.axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
+        for (int j = 0; j < w; j++) pres[(size_t)q * w + j] = P[cell(op.axis, op.idx, j)];
+      }
+      if (!dev_ok(c, hipMemcpyAsync(d_off, off.data(), nb * 8, hipMemcpyHostToDevice, s), "H2D") ||
+          !dev_ok(c, hipMemcpyAsync(d_stride, stride.data(), nb * 8, hipMemcpyHostToDevice, s), "H2D") ||
+          !dev_ok(c, hipMemcpyAsync(d_pres, pres.data(), pres.size(), hipMemcpyHostToDevice, s), "H2D"))
+        return CDA_E_DEVICE;
+      {
+        ProfScope ps(c, "repair_decode", s);
+        const int lr = launch_rs_decode(d_eds, d_off, d_stride, d_pres, nb, K, CDA_SHARE, s);
+        if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+      }
+      // verification: own axis, then orthogonal axes, per operation in order
+      std::vector<int> vaxes;
+      for (size_t q = b0; q < b1; q++) {
+        vaxes.push_back(enc_axis(ops[q].axis, ops[q].idx));
+        for (int o : ops[q].ortho) vaxes.push_back(o);
+      }
+      size_t t = 0;
+      for (size_t v0 = 0; v0 < vaxes.size(); v0 += trees_cap) {  // chunks of at most trees_cap trees
+        std::vector<int> chunk(vaxes.begin() + v0, vaxes.begin() + std::min(vaxes.size(), v0 + trees_cap));
+        if ((rc = roots_of(chunk))) return rc;
+        for (size_t u = 0; u < chunk.size(); u++, t++) {
+          if (root_ok(u, chunk[u])) continue;
+          // locate the operation owning verification t; earlier operations stay applied
+          size_t acc = 0;
+          for (size_t q = b0; q < b1; q++) {
+            const size_t nv = 1 + ops[q].ortho.size();
+            if (t < acc + nv) {
+              for (size_t e = b0; e < q; e++)
+                for (int j = 0; j < w; j++) P[cell(ops[e].axis, ops[e].idx, j)] = 1;
+              const int bad = t == acc ? enc_axis(ops[q].axis, ops[q].idx) : ops[q].ortho[t - acc - 1];
+              return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
+            }
+            acc += nv;
+          }
+        }
+      }
+      for (size_t q = b0; q < b1; q++)
+        for (int j = 0; j < w; j++) P[cell(ops[q].axis, ops[q].idx, j)] = 1;
+      b0 = b1;
+    }
+    if (solved) break;
+    if (!progress) return finish(CDA_E_UNREPAIRABLE, -1, -1);
+  }
+  return finish(CDA_OK, -1, -1);
 }
 
 int cda_profile_enable(cda_ctx* c, int enable) {

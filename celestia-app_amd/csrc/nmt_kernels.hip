@@ -414,6 +414,35 @@ __global__ void __launch_bounds__(256) level_generic_kernel(const uint4* __restr
 }
 
 // ---------------------------------------------------------------------------
+// Roots of an arbitrary list of EDS axes (Repair verification): tree t covers
+// axis axes[t] = (axis << 24) | index over the w cells of that row / column.
+// status[t] gets a non-~0 value if the Push order check fails on that axis.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) axes_leaf_kernel(const uint8_t* __restrict__ eds, int k, int log2w,
+                                                        const int* __restrict__ axes, int ntrees,
+                                                        uint4* __restrict__ nodes,
+                                                        unsigned long long* __restrict__ status) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = 1 << log2w;
+  if (gid >= (uint32_t)ntrees * w) return;
+  const int t = gid >> log2w, i = gid & (w - 1);
+  const int ax = axes[t] >> 24, idx = axes[t] & 0xFFFFFF;
+  const size_t cell = ax == CDA_AXIS_ROW ? ((size_t)idx << log2w) + i : ((size_t)i << log2w) + idx;
+  const bool q0 = (i < k) && (idx < k);
+  const uint4* sh = reinterpret_cast<const uint4*>(eds + cell * CDA_SHARE);
+  uint32_t A[16];
+  load16(sh, A);
+  if (q0 && i + 1 < k) {
+    const size_t nxt = ax == CDA_AXIS_ROW ? cell + 1 : cell + w;
+    const uint4* p = reinterpret_cast<const uint4*>(eds + nxt * CDA_SHARE);
+    uint4 v0 = p[0], v1 = p[1];
+    uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    if (ns_cmp(nb, A) < 0) atomicMin(status + t, (unsigned long long)(i + 1));
+  }
+  leaf_record(sh, A, q0, nodes + (size_t)gid * 6);
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
@@ -461,6 +490,58 @@ int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint6
   if (n <= 0) return 0;
   hipLaunchKernelGGL(axis_leaf_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_leaves, n,
                      (unsigned long long)square_size, (unsigned long long)axis_index, (uint4*)d_nodes, d_status);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int ntrees, void* d_nodes, void* d_scratch,
+                      void* d_roots, unsigned long long* d_status, hipStream_t s) {
+  if (ntrees <= 0) return 0;
+  const int w = 2 * k;
+  int log2w = 0;
+  while ((1 << log2w) < w) log2w++;
+  const uint32_t total = (uint32_t)ntrees * w;
+  hipLaunchKernelGGL(axes_leaf_kernel, dim3((total + 255) / 256), dim3(256), 0, s, d_eds, k, log2w, d_axes, ntrees,
+                     (uint4*)d_nodes, d_status);
+  if (hipGetLastError() != hipSuccess) return -1;
+  void* bufs[2] = {d_nodes, d_scratch};
+  for (int level = 1; level <= log2w; level++) {
+    const int log2n_out = log2w - level;
+    const uint32_t tot = (uint32_t)ntrees << log2n_out;
+    void* out = level == log2w ? d_roots : bufs[level & 1];
+    hipLaunchKernelGGL(nmt_level_kernel<false>, dim3((tot + 255) / 256), dim3(256), 0, s,
+                       (const uint4*)bufs[(level - 1) & 1], (uint4*)out, log2w, log2n_out, tot);
+    if (hipGetLastError() != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+// flags[a] |= 1 if the k parity cells of axis axes[a] differ from par[a][0..k)
+__global__ void __launch_bounds__(256) parity_compare_kernel(const uint8_t* __restrict__ eds, int k, int log2w,
+                                                             const int* __restrict__ axes, int naxes,
+                                                             const uint8_t* __restrict__ par,
+                                                             unsigned* __restrict__ flags) {
+  const size_t per_axis = (size_t)k * (CDA_SHARE / 16);
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= per_axis * naxes) return;
+  const int a = (int)(gid / per_axis);
+  const size_t r = gid % per_axis;
+  const int j = (int)(r / (CDA_SHARE / 16)), q = (int)(r % (CDA_SHARE / 16));
+  const int ax = axes[a] >> 24, idx = axes[a] & 0xFFFFFF;
+  const int i = k + j;
+  const size_t cell = ax == CDA_AXIS_ROW ? ((size_t)idx << log2w) + i : ((size_t)i << log2w) + idx;
+  const uint4 x = reinterpret_cast<const uint4*>(eds + cell * CDA_SHARE)[q];
+  const uint4 y = reinterpret_cast<const uint4*>(par + ((size_t)a * k + j) * CDA_SHARE)[q];
+  if ((x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w)) atomicOr(flags + a, 1u);
+}
+
+int launch_parity_compare(const uint8_t* d_eds, int k, const int* d_axes, int naxes, const uint8_t* d_par,
+                          unsigned* d_flags, hipStream_t s) {
+  if (naxes <= 0) return 0;
+  int log2w = 0;
+  while ((1 << log2w) < 2 * k) log2w++;
+  const size_t total = (size_t)naxes * k * (CDA_SHARE / 16);
+  hipLaunchKernelGGL(parity_compare_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, d_eds, k, log2w,
+                     d_axes, naxes, d_par, d_flags);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -190,3 +190,91 @@ def test_codec_decode_interface(ctx):
     full = data + c.encode(data)
     shards = [s if i in (1, 4, 6, 7) else None for i, s in enumerate(full)]
     assert c.decode(shards) == full
+
+
+# ---- Repair (rsmt2d ExtendedDataSquare.Repair) ----------------------------------------------
+def _square(k, seed):
+    rc, eds, rr, cr, dah = O.extend_commit(O.gen_ods(k, seed))
+    assert rc == 0
+    return eds, rr, cr
+
+
+def _check_repair(ctx, eds, rr, cr, pres):
+    from cda import CdaError
+    damaged = np.where(pres[:, None] == 1, eds, 0xEE).astype(np.uint8)
+    rc_o, eds_o, p_o, ax_o, ix_o = O.repair(damaged, pres, rr, cr)
+    try:
+        got, p_g = ctx.repair(damaged, pres, rr, cr)
+        rc_g, ax_g, ix_g = 0, -1, -1
+    except CdaError as e:
+        rc_g, ax_g, ix_g = e.code, e.axis, e.index
+        got, p_g = None, None
+    assert rc_g == rc_o, (rc_g, rc_o)
+    if rc_o == 0:
+        assert np.array_equal(got, eds) and p_g.all()
+    elif rc_o == O.E_BYZANTINE:
+        assert (ax_g, ix_g) == (ax_o, ix_o)
+    return rc_o
+
+
+@pytest.mark.parametrize("k", [2, 4, 16, 32, 128])
+def test_repair_q0_only(ctx, k):
+    eds, rr, cr = _square(k, 300 + k)
+    w = 2 * k
+    pres = np.zeros((w, w), np.uint8)
+    pres[:k, :k] = 1
+    assert _check_repair(ctx, eds, rr, cr, pres.reshape(-1)) == 0
+
+
+@pytest.mark.parametrize("k,frac", [(8, 0.5), (32, 0.5), (128, 0.5), (128, 0.6), (32, 0.3), (128, 0.25)])
+def test_repair_random(ctx, k, frac):
+    eds, rr, cr = _square(k, 400 + k)
+    rng = np.random.default_rng(k)
+    pres = (rng.random(4 * k * k) < frac).astype(np.uint8)
+    _check_repair(ctx, eds, rr, cr, pres)
+
+
+def test_repair_ff16(ctx):
+    k = 256
+    eds, rr, cr = _square(k, 7)
+    rng = np.random.default_rng(5)
+    pres = (rng.random(4 * k * k) < 0.9).astype(np.uint8)
+    assert _check_repair(ctx, eds, rr, cr, pres) == 0
+
+
+def test_repair_byzantine_complete_row(ctx):
+    k = 8
+    eds, rr, cr = _square(k, 21)
+    w = 2 * k
+    bad = eds.copy()
+    bad[3 * w + 12, 200] ^= 0x10  # parity cell of complete row 3
+    pres = np.ones(w * w, np.uint8)
+    pres[5 * w + 1] = 0
+    _check_repair(ctx, bad, rr, cr, pres)
+
+
+def test_repair_byzantine_during_crossword(ctx):
+    k = 8
+    eds, rr, cr = _square(k, 22)
+    w = 2 * k
+    rng = np.random.default_rng(3)
+    pres = (rng.random(w * w) < 0.6).astype(np.uint8)
+    # corrupt one present cell so that its row/col decode fails verification
+    idx = int(np.flatnonzero(pres)[17])
+    bad = eds.copy()
+    bad[idx, 50] ^= 0xFF
+    rc = _check_repair(ctx, bad, rr, cr, pres)
+    assert rc in (O.E_BYZANTINE, O.E_UNREPAIRABLE)
+
+
+def test_rsmt2d_repair_api(ctx):
+    from cda import rsmt2d
+    k = 4
+    eds, rr, cr = _square(k, 9)
+    cells = [bytes(eds[i]) if (i // (2 * k) < k and i % (2 * k) < k) else None for i in range(4 * k * k)]
+    sq = rsmt2d.import_extended_data_square(cells, rsmt2d.LeoRSCodec(ctx))
+    sq.repair([bytes(r) for r in rr], [bytes(c) for c in cr])
+    assert all(sq.get_cell(i // (2 * k), i % (2 * k)) == bytes(eds[i]) for i in range(4 * k * k))
+    sq2 = rsmt2d.import_extended_data_square([None] * (4 * k * k), rsmt2d.LeoRSCodec(ctx))
+    with pytest.raises(rsmt2d.ErrUnrepairableDataSquare):
+        sq2.repair([bytes(r) for r in rr], [bytes(c) for c in cr])
