@@ -35,9 +35,31 @@ def block_compressions_engine(k):  # each EDS cell hashed once (row & col leaf d
     return 9 * w * w + 3 * (2 * w) * (w - 1) + 2 * (2 * w) + 2 * (2 * w - 1)
 
 
-def leaf_kernel_bytes(k):  # leaf_hash: read every EDS cell, write 90-B leaf nodes
-    w = 2 * k
-    return w * w * (512 + 90)
+def kernel_step_bytes(name, k, B):
+    """Algorithmic HBM bytes one bench step moves through kernel `name` (B blocks of width k).
+
+    rows: read Q0, write the Q0 copy + Q1; cols: read the top half, write the
+    bottom half; leaf_hash: read every EDS cell, write a 90-B leaf node;
+    NMT levels: read 2 child nodes, write 1 (90 B each); dah: read 4k roots.
+    """
+    w, S, N = 2 * k, 512, 90
+    if name.endswith("_rows"):
+        return B * 3 * k * k * S
+    if name.endswith("_cols"):
+        return B * 2 * w * k * S
+    if name == "leaf_hash":
+        return B * w * w * (S + N)
+    if name == "nmt_level1":
+        return B * 2 * w * (w // 2) * 3 * N
+    if name == "nmt_level":  # levels 2..log2(w)
+        n, tot = w // 2, 0
+        while n > 1:
+            tot += 2 * w * (n // 2) * 3 * N
+            n //= 2
+        return B * tot
+    if name == "dah":
+        return B * (2 * w * N + 32)
+    return None
 
 
 def splitmix_bytes(seed, n_u64):
@@ -159,13 +181,18 @@ def main():
     kern = {n: {"avg_ms": ms / max(1, cnt), "launches": cnt, "total_ms": ms} for n, (ms, cnt) in prof.items()}
     dom = max(kern, key=lambda n: kern[n]["total_ms"])
     HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
-    dom_bytes = leaf_kernel_bytes(k) * B if dom == "leaf_hash" else None
-    achieved = (dom_bytes / (kern[dom]["avg_ms"] * 1e-3) / 1e9) if dom_bytes else None
+    dom_step_bytes = kernel_step_bytes(dom, k, B)
+    dom_ms_per_step = kern[dom]["total_ms"] / prof_steps  # = launches/step x avg launch duration
+    achieved = dom_step_bytes / (dom_ms_per_step * 1e-3) / 1e9 if dom_step_bytes else None
     path_gbs = block_bytes(k) * value / world / 1e9
-    # VALU view: SHA-256 compressions (the binding resource)
+    # VALU view: SHA-256 compressions are the binding resource;
+    # ceiling = register-only sha256_compress throughput measured by tools/sha_ubench.hip.
     comp_per_s = block_compressions_engine(k) * value / world
-    VALU_PEAK_OPS = 256 * 128 * 2.4e9  # int32 lane-ops/s (256 CU x 4 SIMD32 x 2.4 GHz)
-    OPS_PER_COMP = 1400  # from the compiled ISA of sha256_compress
+    SHA_CEIL = 28.6e9
+    sha_kernels = [n for n in kern if n in ("leaf_hash", "nmt_level1", "nmt_level")]
+    sha_ms = sum(kern[n]["total_ms"] for n in sha_kernels) / prof_steps
+    sha_comp_step = B * (block_compressions_engine(k) - 2 * (2 * (2 * k)) + 2)  # minus the DAH's
+    sha_rate = sha_comp_step / (sha_ms * 1e-3) if sha_ms else None
 
     result = {
         "metric": "ODS->EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s",
@@ -185,10 +212,19 @@ def main():
                    "k": k, "blocks_per_gpu_per_step": B, "share_size": 512, "parallelism": f"blocks x{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK, 4) if achieved else None, "traffic": None},
+                     "frac": round(achieved / HBM_PEAK, 4) if achieved else None, "traffic": None,
+                     "bytes_per_launch": (dom_step_bytes // max(1, kern[dom]["launches"] // prof_steps))
+                     if dom_step_bytes else None,
+                     "avg_launch_ms": round(kern[dom]["avg_ms"], 4),
+                     "note": "traffic: PMC HBM bytes per launch are in profiles/r01_*_counters.json "
+                             "(rocprofv3 pass, FETCH_SIZE x2 + WRITE_SIZE); the SHA kernels are VALU-bound, "
+                             "see valu_roofline"},
+        "valu_roofline": {"kernels": sha_kernels, "achieved": sha_rate, "peak": SHA_CEIL,
+                          "unit": "SHA-256 compressions/s",
+                          "frac": round(sha_rate / SHA_CEIL, 4) if sha_rate else None,
+                          "peak_source": "tools/sha_ubench.hip register-only sha256_compress on MI355X"},
         "path_hbm_gbs": round(path_gbs, 1),
-        "valu": {"sha256_compressions_per_s": comp_per_s,
-                 "frac_of_int32_peak": round(comp_per_s * OPS_PER_COMP / VALU_PEAK_OPS, 4)},
+        "sha256_compressions_per_s": comp_per_s,
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

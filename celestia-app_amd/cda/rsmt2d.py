@@ -155,7 +155,8 @@ def import_extended_data_square(cells, codec=None):
     """rsmt2d.ImportExtendedDataSquare (flattened row-major, None = missing)."""
     n = len(cells)
     w = int(round(n ** 0.5))
-    L = max(len(c) for c in cells if c is not None)
+    # an all-missing square has no share size to read; use appconsts.ShareSize
+    L = max((len(c) for c in cells if c is not None), default=512)
     arr = np.zeros((n, L), np.uint8)
     present = np.zeros(n, np.uint8)
     for i, c in enumerate(cells):

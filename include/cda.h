@@ -102,7 +102,8 @@ int cda_extend_commit_batch(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const ui
 /* Device-resident form (pointers are device memory of this ctx's GPU; `stream`
  * is a hipStream_t or NULL for the null stream).  Asynchronous: returns after
  * enqueueing; namespace-order errors are reported into the device word
- * `d_status` (int32 per block: 0 ok, else CDA_E_NS_ORDER) for the caller to read.
+ * `d_status` (uint64 per block: all-ones = ok, else the first namespace-order
+ * violation packed as axis << 40 | axis_index << 20 | leaf) for the caller to read.
  * d_roots: nblocks * 4k * 96 bytes (row roots then col roots, 90-B node + 6 zero
  * bytes per record).  d_dah: nblocks * 32. */
 int cda_extend_commit_device(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds,
