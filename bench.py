@@ -112,7 +112,12 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="independent blocks per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["block_batch", "split"], default="block_batch",
+                    help="block_batch: B independent blocks per GPU (default, BASELINE metric); "
+                         "split: ONE k-square split over all ranks with an RCCL all-to-all (config C5, --k 512)")
     args = ap.parse_args()
+    if args.workload == "split":
+        return bench_split(args)
 
     import torch
     import torch.distributed as dist
@@ -229,6 +234,60 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_split(args):
+    """Config C5: one k x k square (k=512: 128 MiB ODS, 512 MiB EDS, GF(2^16)) split over the ranks."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import cda
+    from cda import split
+    ctx = cda.Context(local)
+    ops = split.DeviceOps(ctx)
+    k = args.k
+    (r0, r1), _ = split.plan(k, world, rank)
+    ods = gen_ods(k, 0xC0FFEE).reshape(k, k, 512)
+    rows = torch.from_numpy(np.ascontiguousarray(ods[r0:r1])).to(dev)
+    for _ in range(args.warmup):
+        split.extend_commit_split(ops, k, rows)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = split.extend_commit_split(ops, k, rows)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = args.steps / elapsed
+    result = {
+        "metric": f"ODS->EDS+DAH squares/sec, one k={k} square split over {world} GPU(s)",
+        "value": round(value, 3), "unit": "squares/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (namespace-sorted random shares, SplitMix64 seed 0xC0FFEE)",
+        "config": {"workload": f"split_k{k}: cda.split.extend_commit_split (rows over ranks, one all-to-all, "
+                               f"bottom-row subtree fold)", "k": k, "parallelism": f"rows x{world}"},
+        "dah": out.dah.hex(),
+        "path_hbm_gbs": round(block_bytes(k) * value / world / 1e9, 1),
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()

@@ -41,6 +41,7 @@ EXPORTS = [
     "cda_rs_encode", "cda_rs_decode", "cda_rs_max_chunks", "cda_rs_name", "cda_rs_validate_chunk_size",
     "cda_extend_commit", "cda_extend_commit_batch", "cda_extend_commit_device", "cda_commit_eds",
     "cda_dah_hash", "cda_nmt_axis_root", "cda_repair",
+    "cda_rs_encode_device", "cda_nmt_roots_device", "cda_nmt_fold_device", "cda_dah_device",
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
 ]
 
@@ -89,6 +90,10 @@ def lib():
                 "cda_dah_hash": (I32, [P, U32, P, P, P]),
                 "cda_nmt_axis_root": (I32, [P, U64, U64, U32, U32, P, P, P]),
                 "cda_repair": (I32, [P, U32, P, P, P, P, P]),
+                "cda_rs_encode_device": (I32, [P, U32, U32, U32, P, I64, I64, P, I64, I64, P]),
+                "cda_nmt_roots_device": (I32, [P, U32, P, U32, U32, U32, U32, U32, P, P, P]),
+                "cda_nmt_fold_device": (I32, [P, U32, U32, P, P, P]),
+                "cda_dah_device": (I32, [P, U32, P, P, P]),
                 "cda_profile_enable": (I32, [P, I32]),
                 "cda_profile_read": (I32, [P, P, SZ, P, P, I32]),
                 "cda_profile_reset": (I32, [P]),
@@ -190,6 +195,29 @@ class Context:
         rc = lib().cda_extend_commit_device(self._h, k, nblocks, ctypes.c_void_p(d_ods), ctypes.c_void_p(d_eds),
                                             ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
                                             ctypes.c_void_p(d_status), ctypes.c_void_p(stream or 0))
+        _check(rc, ctx=self)
+
+    # ---- device-resident building blocks (pointers are device addresses) ----
+    def rs_encode_device(self, k, shard_len, ncw, d_src, src_cw, src_sh, d_dst, dst_cw, dst_sh, stream=None):
+        rc = lib().cda_rs_encode_device(self._h, k, shard_len, ncw, ctypes.c_void_p(d_src), src_cw, src_sh,
+                                        ctypes.c_void_p(d_dst), dst_cw, dst_sh, ctypes.c_void_p(stream or 0))
+        _check(rc, ctx=self)
+
+    def nmt_roots_device(self, k, d_eds, axis, first_index, naxes, leaf_off, nleaves, d_roots, d_status,
+                         stream=None):
+        rc = lib().cda_nmt_roots_device(self._h, k, ctypes.c_void_p(d_eds), axis, first_index, naxes, leaf_off,
+                                        nleaves, ctypes.c_void_p(d_roots), ctypes.c_void_p(d_status),
+                                        ctypes.c_void_p(stream or 0))
+        _check(rc, ctx=self)
+
+    def nmt_fold_device(self, ntrees, n, d_nodes, d_roots, stream=None):
+        rc = lib().cda_nmt_fold_device(self._h, ntrees, n, ctypes.c_void_p(d_nodes), ctypes.c_void_p(d_roots),
+                                       ctypes.c_void_p(stream or 0))
+        _check(rc, ctx=self)
+
+    def dah_device(self, n_total, d_roots, d_dah, stream=None):
+        rc = lib().cda_dah_device(self._h, n_total, ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
+                                  ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
 
     def commit_eds(self, eds):

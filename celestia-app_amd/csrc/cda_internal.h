@@ -60,9 +60,13 @@ int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks,
 int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,
                      unsigned long long* d_status, hipStream_t s);
 int launch_level_generic(const void* d_in, void* d_out, int n_in, hipStream_t s);
-// roots of ntrees EDS axes (axes[t] = axis << 24 | index), 96-B records into d_roots
-int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int ntrees, void* d_nodes, void* d_scratch,
-                      void* d_roots, unsigned long long* d_status, hipStream_t s);
+// roots of ntrees EDS axes (code_t = d_axes ? d_axes[t] : axis0 + t, code = axis << 24 | index) over
+// leaves [leaf_off, leaf_off + nleaves) (nleaves a power of two, leaf_off a multiple of it), 96-B
+// records into d_roots; d_nodes / d_scratch hold ntrees * nleaves records each.  -2: bad range.
+int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int axis0, int ntrees, int leaf_off, int nleaves,
+                      void* d_nodes, void* d_scratch, void* d_roots, unsigned long long* d_status, hipStream_t s);
+// ntrees x 2^log2n contiguous 96-B node records -> ntrees roots (d_nodes is overwritten)
+int launch_nmt_fold(void* d_nodes, void* d_scratch, void* d_roots, int ntrees, int log2n, hipStream_t s);
 int launch_parity_compare(const uint8_t* d_eds, int k, const int* d_axes, int naxes, const uint8_t* d_par,
                           unsigned* d_flags, hipStream_t s);
 

@@ -412,6 +412,78 @@ int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const voi
                           (unsigned long long*)d_status, s);
 }
 
+int cda_rs_encode_device(cda_ctx* c, uint32_t k, uint32_t shard_len, uint32_t ncw, const void* d_src, int64_t src_cw,
+                         int64_t src_sh, void* d_dst, int64_t dst_cw, int64_t dst_sh, void* stream) {
+  if (!c || !d_src || !d_dst || k == 0 || k > 32768) return CDA_E_ARG;
+  if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
+  if (ncw == 0) return CDA_OK;
+  Lock l(c);
+  hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  RsJob j{};
+  j.src = (const uint8_t*)d_src;
+  j.src_cw = src_cw;
+  j.src_sh = src_sh;
+  j.dst = (uint8_t*)d_dst;
+  j.dst_cw = dst_cw;
+  j.dst_sh = dst_sh;
+  j.k = (int)k;
+  j.cw_per_blk = (int)ncw;
+  j.nblk = 1;
+  j.shard_len = (int)shard_len;
+  ProfScope ps(c, 2 * k <= 256 ? "rs_encode8" : "rs_encode16", s);
+  const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
+  if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+  return CDA_OK;
+}
+
+int cda_nmt_roots_device(cda_ctx* c, uint32_t k, const void* d_eds, uint32_t axis, uint32_t first_index,
+                         uint32_t naxes, uint32_t leaf_off, uint32_t nleaves, void* d_roots, void* d_status,
+                         void* stream) {
+  if (!c || !d_eds || !d_roots || !d_status || (axis != CDA_AXIS_ROW && axis != CDA_AXIS_COL)) return CDA_E_ARG;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  const uint32_t w = 2 * k;
+  if (k > kMaxDeviceK || first_index + naxes > w || !is_pow2(nleaves) || leaf_off % nleaves || leaf_off + nleaves > w)
+    return CDA_E_ARG;
+  if (naxes == 0) return CDA_OK;
+  Lock l(c);
+  hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  const size_t recs = (size_t)naxes * nleaves * CDA_REC_BYTES;
+  int rc;
+  if ((rc = ensure(c, c->leaf, recs)) || (rc = ensure(c, c->scratch, recs))) return rc;
+  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)naxes * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+  ProfScope ps(c, "nmt_roots", s);
+  const int lr = launch_axes_roots((const uint8_t*)d_eds, (int)k, nullptr, (int)((axis << 24) | first_index),
+                                   (int)naxes, (int)leaf_off, (int)nleaves, c->leaf.p, c->scratch.p, d_roots,
+                                   (unsigned long long*)d_status, s);
+  if (lr) return lr == -2 ? CDA_E_ARG : CDA_E_DEVICE;
+  return CDA_OK;
+}
+
+int cda_nmt_fold_device(cda_ctx* c, uint32_t ntrees, uint32_t n, const void* d_nodes, void* d_roots, void* stream) {
+  if (!c || !d_nodes || !d_roots || !is_pow2(n)) return CDA_E_ARG;
+  if (ntrees == 0) return CDA_OK;
+  Lock l(c);
+  hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  const size_t bytes = (size_t)ntrees * n * CDA_REC_BYTES;
+  if (n == 1) return dev_ok(c, hipMemcpyAsync(d_roots, d_nodes, bytes, hipMemcpyDeviceToDevice, s), "D2D") ? CDA_OK
+                                                                                                          : CDA_E_DEVICE;
+  int rc;
+  if ((rc = ensure(c, c->leaf, bytes)) || (rc = ensure(c, c->scratch, bytes))) return rc;
+  if (!dev_ok(c, hipMemcpyAsync(c->leaf.p, d_nodes, bytes, hipMemcpyDeviceToDevice, s), "D2D")) return CDA_E_DEVICE;
+  ProfScope ps(c, "nmt_fold", s);
+  return launch_nmt_fold(c->leaf.p, c->scratch.p, d_roots, (int)ntrees, ilog2i(n), s) ? CDA_E_DEVICE : CDA_OK;
+}
+
+int cda_dah_device(cda_ctx* c, uint32_t n_total, const void* d_roots, void* d_dah, void* stream) {
+  if (!c || !d_roots || !d_dah || n_total == 0) return CDA_E_ARG;
+  Lock l(c);
+  hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  ProfScope ps(c, "dah", s);
+  const int lr = launch_dah(d_roots, d_dah, (int)n_total, 1, s);
+  if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+  return CDA_OK;
+}
+
 int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
                             uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
   set_err(err, CDA_OK, -1, -1, -1, -1);
@@ -663,7 +735,7 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
       return CDA_E_DEVICE;
     {
       ProfScope ps(c, "repair_roots", s);
-      if (launch_axes_roots(d_eds, K, d_axes, (int)axes.size(), c->leaf.p, c->scratch.p, c->roots.p,
+      if (launch_axes_roots(d_eds, K, d_axes, 0, (int)axes.size(), 0, w, c->leaf.p, c->scratch.p, c->roots.p,
                             (unsigned long long*)c->status.p, s))
         return CDA_E_DEVICE;
     }

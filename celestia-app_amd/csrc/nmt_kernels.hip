@@ -414,19 +414,23 @@ __global__ void __launch_bounds__(256) level_generic_kernel(const uint4* __restr
 }
 
 // ---------------------------------------------------------------------------
-// Roots of an arbitrary list of EDS axes (Repair verification): tree t covers
-// axis axes[t] = (axis << 24) | index over the w cells of that row / column.
-// status[t] gets a non-~0 value if the Push order check fails on that axis.
+// Roots of a list of EDS axes (Repair verification, split-square path): tree t
+// covers axis code a_t = axes ? axes[t] : axis0 + t  ((axis << 24) | index),
+// leaves [leaf_off, leaf_off + 2^log2n) of that row / column.  With the full
+// range this is the axis root; with an aligned power-of-two sub-range it is the
+// root of that subtree (the NMT splits at powers of two, nmt_wrapper.go:118).
+// status[t] gets the first leaf index whose Push order check fails.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) axes_leaf_kernel(const uint8_t* __restrict__ eds, int k, int log2w,
-                                                        const int* __restrict__ axes, int ntrees,
-                                                        uint4* __restrict__ nodes,
+                                                        const int* __restrict__ axes, int axis0, int ntrees,
+                                                        int leaf_off, int log2n, uint4* __restrict__ nodes,
                                                         unsigned long long* __restrict__ status) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int w = 1 << log2w;
-  if (gid >= (uint32_t)ntrees * w) return;
-  const int t = gid >> log2w, i = gid & (w - 1);
-  const int ax = axes[t] >> 24, idx = axes[t] & 0xFFFFFF;
+  if (gid >= ((uint32_t)ntrees << log2n)) return;
+  const int t = gid >> log2n, i = leaf_off + (int)(gid & ((1u << log2n) - 1));
+  const int code = axes ? axes[t] : axis0 + t;
+  const int ax = code >> 24, idx = code & 0xFFFFFF;
   const size_t cell = ax == CDA_AXIS_ROW ? ((size_t)idx << log2w) + i : ((size_t)i << log2w) + idx;
   const bool q0 = (i < k) && (idx < k);
   const uint4* sh = reinterpret_cast<const uint4*>(eds + cell * CDA_SHARE);
@@ -493,23 +497,31 @@ int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint6
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int ntrees, void* d_nodes, void* d_scratch,
-                      void* d_roots, unsigned long long* d_status, hipStream_t s) {
+int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int axis0, int ntrees, int leaf_off, int nleaves,
+                      void* d_nodes, void* d_scratch, void* d_roots, unsigned long long* d_status, hipStream_t s) {
   if (ntrees <= 0) return 0;
-  const int w = 2 * k;
-  int log2w = 0;
-  while ((1 << log2w) < w) log2w++;
-  const uint32_t total = (uint32_t)ntrees * w;
-  hipLaunchKernelGGL(axes_leaf_kernel, dim3((total + 255) / 256), dim3(256), 0, s, d_eds, k, log2w, d_axes, ntrees,
-                     (uint4*)d_nodes, d_status);
+  int log2w = 0, log2n = 0;
+  while ((1 << log2w) < 2 * k) log2w++;
+  while ((1 << log2n) < nleaves) log2n++;
+  if ((1 << log2n) != nleaves || leaf_off < 0 || leaf_off % nleaves || leaf_off + nleaves > 2 * k) return -2;
+  const uint32_t total = (uint32_t)ntrees << log2n;
+  hipLaunchKernelGGL(axes_leaf_kernel, dim3((total + 255) / 256), dim3(256), 0, s, d_eds, k, log2w, d_axes, axis0,
+                     ntrees, leaf_off, log2n, (uint4*)(log2n == 0 ? d_roots : d_nodes), d_status);
   if (hipGetLastError() != hipSuccess) return -1;
+  return launch_nmt_fold(d_nodes, d_scratch, d_roots, ntrees, log2n, s);
+}
+
+// ntrees x 2^log2n contiguous node records -> ntrees roots (levels ping-pong
+// between `nodes` and `scratch`; the last level writes `roots`).
+int launch_nmt_fold(void* d_nodes, void* d_scratch, void* d_roots, int ntrees, int log2n, hipStream_t s) {
   void* bufs[2] = {d_nodes, d_scratch};
-  for (int level = 1; level <= log2w; level++) {
-    const int log2n_out = log2w - level;
+  for (int level = 1; level <= log2n; level++) {
+    const int log2n_out = log2n - level;
     const uint32_t tot = (uint32_t)ntrees << log2n_out;
-    void* out = level == log2w ? d_roots : bufs[level & 1];
+    void* out = level == log2n ? d_roots : bufs[level & 1];
+    // nmt_level_kernel<false>'s log2w argument only sizes the tree: trees of 2^log2n leaves
     hipLaunchKernelGGL(nmt_level_kernel<false>, dim3((tot + 255) / 256), dim3(256), 0, s,
-                       (const uint4*)bufs[(level - 1) & 1], (uint4*)out, log2w, log2n_out, tot);
+                       (const uint4*)bufs[(level - 1) & 1], (uint4*)out, log2n, log2n_out, tot);
     if (hipGetLastError() != hipSuccess) return -1;
   }
   return 0;

@@ -109,6 +109,38 @@ int cda_extend_commit_batch(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const ui
 int cda_extend_commit_device(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds,
                              void* d_roots, void* d_dah, void* d_status, void* stream);
 
+/* ---- device-resident building blocks (one square split over GPUs) ----
+ * All pointers are device memory of this ctx's GPU; asynchronous on `stream`
+ * (hipStream_t or NULL).  They share the ctx's scratch workspace, so calls on
+ * different streams of one ctx must be ordered by the caller. */
+
+/* Batched strided Codec.Encode: for codeword c < ncw, data shard i at
+ * d_src + c*src_cw + i*src_sh, parity shard i written to d_dst + c*dst_cw + i*dst_sh
+ * (byte strides).  The rows of rsmt2d erasureExtendSquare are (src_cw = row
+ * pitch, src_sh = shard_len), its columns (src_cw = shard_len, src_sh = row pitch). */
+int cda_rs_encode_device(cda_ctx* ctx, uint32_t k, uint32_t shard_len, uint32_t ncw, const void* d_src, int64_t src_cw,
+                         int64_t src_sh, void* d_dst, int64_t dst_cw, int64_t dst_sh, void* stream);
+
+/* Erasured-NMT roots of `naxes` consecutive axes (axis = CDA_AXIS_ROW/COL,
+ * indices first_index ..) of a 2k x 2k row-major EDS `d_eds` (512-B shares; only
+ * the cells read are needed), over leaves [leaf_off, leaf_off + nleaves):
+ * nleaves = 2k gives the axis root (eds.RowRoots / ColRoots, nmt_wrapper.go:118-124);
+ * an aligned power-of-two sub-range gives the root of that subtree, which the
+ * split-square path folds across GPUs.  d_roots: naxes 96-B records (90-B node +
+ * 6 zero bytes).  d_status: naxes uint64, all-ones or the first leaf index whose
+ * Push order check failed (nmt ErrInvalidPushOrder). */
+int cda_nmt_roots_device(cda_ctx* ctx, uint32_t k, const void* d_eds, uint32_t axis, uint32_t first_index,
+                         uint32_t naxes, uint32_t leaf_off, uint32_t nleaves, void* d_roots, void* d_status,
+                         void* stream);
+
+/* ntrees x n (power of two) contiguous 96-B node records -> ntrees root records
+ * (NmtHasher.HashNode levels, test/util/malicious/hasher.go:271-310). */
+int cda_nmt_fold_device(cda_ctx* ctx, uint32_t ntrees, uint32_t n, const void* d_nodes, void* d_roots, void* stream);
+
+/* DataAvailabilityHeader.Hash over n_total 96-B root records (row roots then
+ * column roots) -> 32 B (pkg/da/data_availability_header.go:92-108). */
+int cda_dah_device(cda_ctx* ctx, uint32_t n_total, const void* d_roots, void* d_dah, void* stream);
+
 /* Roots + DAH of an existing EDS (rsmt2d eds.RowRoots/ColRoots + DAH hash). */
 int cda_commit_eds(cda_ctx* ctx, uint32_t k, const uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots,
                    uint8_t* dah, cda_err_info* err);
