@@ -11,6 +11,7 @@
 //   5. dah                  : RFC-6962 over row roots ‖ col roots
 // Nothing here computes on the CPU: the host only validates arguments, moves
 // buffers and maps device status words to error codes.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,6 +37,12 @@ struct cda_ctx {
   int nsub = 4;
   hipStream_t sub[kMaxSub] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
+  // CU-partitioned pipeline (CDA_CU_SPLIT = CUs given to RS): the memory-bound RS
+  // phase of chunk i+1 runs on its own CUs while the VALU-bound SHA phase of
+  // chunk i runs on the rest.
+  int cu_split = 0, pipe_chunks = 4;
+  hipStream_t rs_stream = nullptr, sha_stream = nullptr;
+  hipEvent_t rs_ev[kMaxSub] = {};
   std::string last_err;
   // workspace
   struct Buf {
@@ -141,8 +148,8 @@ void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block
 
 // Enqueue the whole block pipeline for blocks [0, nblocks) of the given buffers,
 // using leaf/scratch records starting at record offset `rec_off`.
-int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
-                         void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
+// RS phase: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
+int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s) {
   const uint32_t w = 2 * k;
   const long long S = CDA_SHARE;
   {
@@ -186,6 +193,13 @@ int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t
     const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
     if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
+  return CDA_OK;
+}
+
+// Commitment phase: leaf hashing, NMT levels, DAH of nblocks extended blocks.
+int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
+                   unsigned long long* d_status, hipStream_t s, size_t rec_off) {
+  const uint32_t w = 2 * k;
   if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
   {
     ProfScope ps(c, "leaf_hash", s);
@@ -207,9 +221,17 @@ int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t
   return CDA_OK;
 }
 
-// Pipeline over nblocks: split into up to c->nsub sub-batches on internal
-// streams forked from / joined back into `s` (serial when profiling so that the
-// per-kernel event timings are not overlapped).
+int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
+                         void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
+  if (int rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s)) return rc;
+  return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, rec_off);
+}
+
+// Pipeline over nblocks.  Default: one stream.  With CU partitioning (cu_split >
+// 0, not while profiling), the batch is cut into chunks; RS of every chunk runs
+// on rs_stream (its own CUs), the commitment of chunk i on sha_stream (the other
+// CUs) after RS(i) -- so RS(i+1) overlaps commit(i).  Otherwise, with nsub > 1,
+// chunks go to independent sub-streams.
 int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                      void* d_dah, unsigned long long* d_status, hipStream_t s) {
   const uint32_t w = 2 * k;
@@ -218,6 +240,32 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (rc) return rc;
   rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
   if (rc) return rc;
+  if (c->rs_stream && !c->prof && nblocks > 1) {
+    const int nch = (int)std::min<uint32_t>((uint32_t)c->pipe_chunks, nblocks);
+    if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
+        !dev_ok(c, hipStreamWaitEvent(c->rs_stream, c->fork_ev, 0), "hipStreamWaitEvent") ||
+        !dev_ok(c, hipStreamWaitEvent(c->sha_stream, c->fork_ev, 0), "hipStreamWaitEvent"))
+      return CDA_E_DEVICE;
+    uint32_t done = 0;
+    for (int i = 0; i < nch; i++) {
+      const uint32_t nb = (nblocks - done) / (uint32_t)(nch - i);
+      if ((rc = enqueue_rs(c, k, nb, d_ods + (size_t)done * k * k * CDA_SHARE, d_eds + (size_t)done * w * w * CDA_SHARE,
+                           c->rs_stream)))
+        return rc;
+      if (!dev_ok(c, hipEventRecord(c->rs_ev[i], c->rs_stream), "hipEventRecord") ||
+          !dev_ok(c, hipStreamWaitEvent(c->sha_stream, c->rs_ev[i], 0), "hipStreamWaitEvent"))
+        return CDA_E_DEVICE;
+      if ((rc = enqueue_commit(c, k, nb, d_eds + (size_t)done * w * w * CDA_SHARE,
+                               (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES, (uint8_t*)d_dah + (size_t)done * 32,
+                               d_status + done, c->sha_stream, (size_t)done * w * w)))
+        return rc;
+      done += nb;
+    }
+    if (!dev_ok(c, hipEventRecord(c->join_ev[0], c->sha_stream), "hipEventRecord") ||
+        !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[0], 0), "hipStreamWaitEvent"))
+      return CDA_E_DEVICE;
+    return CDA_OK;
+  }
   const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
   if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
   if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
@@ -277,10 +325,28 @@ int cda_init(int device, cda_ctx** out) {
     return CDA_E_DEVICE;
   }
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
+  if (const char* e = getenv("CDA_CU_SPLIT")) c->cu_split = std::max(0, atoi(e));
+  if (const char* e = getenv("CDA_PIPE_CHUNKS")) c->pipe_chunks = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
     ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->rs_ev[i], hipEventDisableTiming) == hipSuccess;
+  if (ok && c->cu_split > 0) {
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    if (ncu > 0 && c->cu_split < ncu) {
+      // spread each partition evenly over the CU numbering (and so over the XCDs)
+      std::vector<uint32_t> rs_mask((ncu + 31) / 32, 0u), sha_mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; i++) {
+        const bool rs = (long long)(i + 1) * c->cu_split / ncu > (long long)i * c->cu_split / ncu;
+        (rs ? rs_mask : sha_mask)[i / 32] |= 1u << (i % 32);
+      }
+      ok = hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()) == hipSuccess &&
+           hipExtStreamCreateWithCUMask(&c->sha_stream, (uint32_t)sha_mask.size(), sha_mask.data()) == hipSuccess;
+      if (!ok) fprintf(stderr, "cda_init: hipExtStreamCreateWithCUMask failed\n");
+    }
+  }
   if (!ok) {
     delete c;
     return CDA_E_DEVICE;
@@ -302,7 +368,10 @@ void cda_free(cda_ctx* c) {
     for (int i = 0; i < cda_ctx::kMaxSub; i++) {
       if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
+      if (c->rs_ev[i]) (void)hipEventDestroy(c->rs_ev[i]);
     }
+    if (c->rs_stream) (void)hipStreamDestroy(c->rs_stream);
+    if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     (void)hipStreamDestroy(c->stream);
   }
