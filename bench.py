@@ -43,6 +43,8 @@ def kernel_step_bytes(name, k, B):
     NMT levels: read 2 child nodes, write 1 (90 B each); dah: read 4k roots.
     """
     w, S, N = 2 * k, 512, 90
+    if name == "fused_rs_leaf":  # rows + cols + leaf hashing in one software-pipelined kernel
+        return sum(kernel_step_bytes(n, k, B) for n in ("x_rows", "x_cols", "leaf_hash"))
     if name.endswith("_rows"):
         return B * 3 * k * k * S
     if name.endswith("_cols"):
@@ -84,23 +86,71 @@ def gen_ods(k, seed):
     return np.sort(v).view(np.uint8).reshape(n, 512)
 
 
+def _host_cpu():
+    model, flags = "unknown", []
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and model == "unknown":
+                model = line.split(":", 1)[1].strip()
+            if line.startswith("flags") and not flags:
+                f = line.split(":", 1)[1].split()
+                flags = [x for x in ("avx2", "avx512f", "gfni", "sha_ni", "vaes") if x in f]
+    except OSError:
+        pass
+    return model, flags
+
+
 def cpu_baseline(k, min_seconds):
-    """The CPU restatement (oracle/, 'port') on this host: bounded sample of k-blocks."""
+    """The CPU restatement (oracle/, 'port') on this host: bounded samples of k-blocks, all-thread and 1-thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1))
     ods = gen_ods(k, 0xC0FFEE)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        rc, *_ = O.extend_commit(ods, want_eds=True, nthreads=threads)
-        assert rc == 0
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds:
-            break
+
+    def rate(nthreads, seconds):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            rc, *_ = O.extend_commit(ods, want_eds=True, nthreads=nthreads)
+            assert rc == 0
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return n, el
+
+    n, el = rate(threads, min_seconds)
+    n1, el1 = rate(1, max(2.0, min_seconds / 3))
+    model, flags = _host_cpu()
     return {"value": n / el, "unit": "blocks/s", "cores": threads, "kind": "port",
+            "single_thread_value": n1 / el1,
+            "host": {"cpu": model, "simd": flags, "os_cpus": os.cpu_count()},
             "sample": f"{n} x k={k} ExtendShares+NewDataAvailabilityHeader via oracle/liboracle.so "
-                      f"(C restatement, OpenSSL SHA-256, AVX2 Leopard), {threads} threads, {el:.1f} s"}
+                      f"(C restatement, OpenSSL SHA-256, AVX2 Leopard; not the Go reference), {threads} threads, "
+                      f"{el:.1f} s; 1 thread: {n1} blocks in {el1:.1f} s"}
+
+
+def repair_measure(ctx, k=128, survive=0.5, reps=3):
+    """Config C4: rsmt2d Repair of a k=128 EDS from a random `survive` fraction of cells (host buffers in/out)."""
+    import cda
+    w = 2 * k
+    ods = gen_ods(k, 0xC0FFEE).reshape(k * k, 512)
+    eds, rr, cr, _ = ctx.extend_commit(ods)
+    rng = np.random.default_rng(7)
+    ms = []
+    for _ in range(reps):
+        present = (rng.random(w * w) < survive).astype(np.uint8)
+        damaged = eds.copy()
+        damaged[present == 0] = 0
+        t0 = time.perf_counter()
+        try:
+            out, _ = ctx.repair(damaged, present, rr, cr)
+            ok = True
+        except cda.CdaError:
+            ok = False
+        ms.append((time.perf_counter() - t0) * 1e3)
+        if ok and not np.array_equal(out, eds):
+            raise RuntimeError("repair produced a different EDS")
+    return {"k": k, "survive": survive, "ms": round(min(ms), 2), "repaired": ok,
+            "note": "cda_repair incl. 32 MiB H2D + D2H of the EDS; PCIe-inclusive"}
 
 
 def main():
@@ -109,7 +159,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128)
-    ap.add_argument("--batch", type=int, default=32, help="independent blocks per GPU per step")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="independent blocks per GPU per step (128 = config C3: 1024 blocks over 8 GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["block_batch", "split"], default="block_batch",
@@ -194,7 +245,7 @@ def main():
     # ceiling = register-only sha256_compress throughput measured by tools/sha_ubench.hip.
     comp_per_s = block_compressions_engine(k) * value / world
     SHA_CEIL = 28.6e9
-    sha_kernels = [n for n in kern if n in ("leaf_hash", "nmt_level1", "nmt_level")]
+    sha_kernels = [n for n in kern if n in ("leaf_hash", "nmt_level1", "nmt_level", "fused_rs_leaf")]
     sha_ms = sum(kern[n]["total_ms"] for n in sha_kernels) / prof_steps
     sha_comp_step = B * (block_compressions_engine(k) - 2 * (2 * (2 * k)) + 2)  # minus the DAH's
     sha_rate = sha_comp_step / (sha_ms * 1e-3) if sha_ms else None
@@ -233,6 +284,7 @@ def main():
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["repair_c4"] = repair_measure(ctx)
         result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

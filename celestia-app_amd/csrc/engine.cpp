@@ -11,7 +11,6 @@
 //   5. dah                  : RFC-6962 over row roots ‖ col roots
 // Nothing here computes on the CPU: the host only validates arguments, moves
 // buffers and maps device status words to error codes.
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,15 +33,11 @@ struct cda_ctx {
   // that one sub-batch's memory-bound RS phase and latency-bound tree tail overlap
   // another's hashing (no dependency between blocks).
   static constexpr int kMaxSub = 8;
-  int nsub = 4;
+  int nsub = 1;
+  // fused k = 128 pipeline (CDA_FUSED=0 disables) over `chunks` chunks (CDA_CHUNKS)
+  int fused = 1, chunks = 4;
   hipStream_t sub[kMaxSub] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
-  // CU-partitioned pipeline (CDA_CU_SPLIT = CUs given to RS): the memory-bound RS
-  // phase of chunk i+1 runs on its own CUs while the VALU-bound SHA phase of
-  // chunk i runs on the rest.
-  int cu_split = 0, pipe_chunks = 4;
-  hipStream_t rs_stream = nullptr, sha_stream = nullptr;
-  hipEvent_t rs_ev[kMaxSub] = {};
   std::string last_err;
   // workspace
   struct Buf {
@@ -149,46 +144,58 @@ void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block
 // Enqueue the whole block pipeline for blocks [0, nblocks) of the given buffers,
 // using leaf/scratch records starting at record offset `rec_off`.
 // RS phase: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
-int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s) {
+RsJob rows_job(uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds) {
   const uint32_t w = 2 * k;
   const long long S = CDA_SHARE;
+  RsJob j{};
+  j.src = d_ods;
+  j.src_blk = (long long)k * k * S;
+  j.src_cw = (long long)k * S;
+  j.src_sh = S;
+  j.dst = d_eds + (size_t)k * S;
+  j.dst_blk = (long long)w * w * S;
+  j.dst_cw = (long long)w * S;
+  j.dst_sh = S;
+  j.cpy = d_eds;
+  j.cpy_blk = j.dst_blk;
+  j.cpy_cw = j.dst_cw;
+  j.cpy_sh = S;
+  j.k = (int)k;
+  j.cw_per_blk = (int)k;
+  j.nblk = (int)nblocks;
+  j.shard_len = CDA_SHARE;
+  return j;
+}
+
+RsJob cols_job(uint32_t k, uint32_t nblocks, uint8_t* d_eds) {
+  const uint32_t w = 2 * k;
+  const long long S = CDA_SHARE;
+  RsJob j{};
+  j.src = d_eds;
+  j.src_blk = (long long)w * w * S;
+  j.src_cw = S;
+  j.src_sh = (long long)w * S;
+  j.dst = d_eds + (size_t)k * w * S;
+  j.dst_blk = j.src_blk;
+  j.dst_cw = S;
+  j.dst_sh = (long long)w * S;
+  j.cpy = nullptr;
+  j.k = (int)k;
+  j.cw_per_blk = (int)w;
+  j.nblk = (int)nblocks;
+  j.shard_len = CDA_SHARE;
+  return j;
+}
+
+int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s) {
   {
-    RsJob j{};
-    j.src = d_ods;
-    j.src_blk = (long long)k * k * S;
-    j.src_cw = (long long)k * S;
-    j.src_sh = S;
-    j.dst = d_eds + (size_t)k * S;
-    j.dst_blk = (long long)w * w * S;
-    j.dst_cw = (long long)w * S;
-    j.dst_sh = S;
-    j.cpy = d_eds;
-    j.cpy_blk = j.dst_blk;
-    j.cpy_cw = j.dst_cw;
-    j.cpy_sh = S;
-    j.k = (int)k;
-    j.cw_per_blk = (int)k;
-    j.nblk = (int)nblocks;
-    j.shard_len = CDA_SHARE;
+    const RsJob j = rows_job(k, nblocks, d_ods, d_eds);
     ProfScope ps(c, 2 * k <= 256 ? "rs_encode8_rows" : "rs_encode16_rows", s);
     const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
     if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   {
-    RsJob j{};
-    j.src = d_eds;
-    j.src_blk = (long long)w * w * S;
-    j.src_cw = S;
-    j.src_sh = (long long)w * S;
-    j.dst = d_eds + (size_t)k * w * S;
-    j.dst_blk = j.src_blk;
-    j.dst_cw = S;
-    j.dst_sh = (long long)w * S;
-    j.cpy = nullptr;
-    j.k = (int)k;
-    j.cw_per_blk = (int)w;
-    j.nblk = (int)nblocks;
-    j.shard_len = CDA_SHARE;
+    const RsJob j = cols_job(k, nblocks, d_eds);
     ProfScope ps(c, 2 * k <= 256 ? "rs_encode8_cols" : "rs_encode16_cols", s);
     const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
     if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
@@ -197,14 +204,9 @@ int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, u
 }
 
 // Commitment phase: leaf hashing, NMT levels, DAH of nblocks extended blocks.
-int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
-                   unsigned long long* d_status, hipStream_t s, size_t rec_off) {
+// NMT levels + DAH of nblocks blocks whose leaf records are at record offset rec_off.
+int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void* d_dah, hipStream_t s, size_t rec_off) {
   const uint32_t w = 2 * k;
-  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
-  {
-    ProfScope ps(c, "leaf_hash", s);
-    if (launch_leaf_hash(d_eds, bufs0(c, rec_off), d_status, (int)k, (int)nblocks, s)) return CDA_E_DEVICE;
-  }
   const int L = ilog2i(w);
   void* bufs[2] = {(uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES, (uint8_t*)c->scratch.p + rec_off * CDA_REC_BYTES};
   for (int level = 1; level <= L; level++) {
@@ -221,17 +223,79 @@ int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ed
   return CDA_OK;
 }
 
+int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
+                   unsigned long long* d_status, hipStream_t s, size_t rec_off) {
+  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+  {
+    ProfScope ps(c, "leaf_hash", s);
+    if (launch_leaf_hash(d_eds, bufs0(c, rec_off), d_status, (int)k, (int)nblocks, s)) return CDA_E_DEVICE;
+  }
+  return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, rec_off);
+}
+
+// k = 128 software pipeline over chunks of blocks: launch t runs rows(chunk t),
+// cols(chunk t-1) and leaf hashing (chunk t-2) in one fused kernel; the NMT
+// levels + DAH of a chunk follow on sub-stream 0 once its leaves are done, so
+// they overlap the next fused launch.
+int enqueue_pipeline_fused(cda_ctx* c, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
+                           void* d_dah, unsigned long long* d_status, hipStream_t s) {
+  const uint32_t k = 128, w = 256;
+  const int nch = (int)std::min<uint32_t>((uint32_t)c->chunks, nblocks);
+  uint32_t first[cda_ctx::kMaxSub + 1];
+  for (int i = 0; i <= nch; i++) first[i] = (uint32_t)((unsigned long long)nblocks * i / nch);
+  auto nb = [&](int i) { return first[i + 1] - first[i]; };
+  auto ods = [&](int i) { return d_ods + (size_t)first[i] * k * k * CDA_SHARE; };
+  auto eds = [&](int i) { return d_eds + (size_t)first[i] * w * w * CDA_SHARE; };
+  hipStream_t t_s = c->prof ? s : c->sub[0];
+  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+  if (t_s != s && (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
+                   !dev_ok(c, hipStreamWaitEvent(t_s, c->fork_ev, 0), "hipStreamWaitEvent")))
+    return CDA_E_DEVICE;
+  for (int t = 0; t < nch + 2; t++) {
+    RsJob rj, cj;
+    const RsJob* rp = nullptr;
+    const RsJob* cp = nullptr;
+    if (t < nch) {
+      rj = rows_job(k, nb(t), ods(t), eds(t));
+      rp = &rj;
+    }
+    if (t >= 1 && t - 1 < nch) {
+      cj = cols_job(k, nb(t - 1), eds(t - 1));
+      cp = &cj;
+    }
+    const int lc = t - 2;
+    {
+      ProfScope ps(c, "fused_rs_leaf", s);
+      const int lr = launch_fused_rs_leaf(rp, cp, lc >= 0 ? eds(lc) : nullptr,
+                                          lc >= 0 ? bufs0(c, (size_t)first[lc] * w * w) : nullptr,
+                                          lc >= 0 ? d_status + first[lc] : nullptr, lc >= 0 ? (int)nb(lc) : 0, s);
+      if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+    }
+    if (lc < 0) continue;
+    if (t_s != s && (!dev_ok(c, hipEventRecord(c->join_ev[lc % cda_ctx::kMaxSub], s), "hipEventRecord") ||
+                     !dev_ok(c, hipStreamWaitEvent(t_s, c->join_ev[lc % cda_ctx::kMaxSub], 0), "hipStreamWaitEvent")))
+      return CDA_E_DEVICE;
+    if (int rc = enqueue_trees(c, k, nb(lc), (uint8_t*)d_roots + (size_t)first[lc] * 2 * w * CDA_REC_BYTES,
+                               (uint8_t*)d_dah + (size_t)first[lc] * 32, t_s, (size_t)first[lc] * w * w))
+      return rc;
+  }
+  if (t_s != s && (!dev_ok(c, hipEventRecord(c->fork_ev, t_s), "hipEventRecord") ||
+                   !dev_ok(c, hipStreamWaitEvent(s, c->fork_ev, 0), "hipStreamWaitEvent")))
+    return CDA_E_DEVICE;
+  return CDA_OK;
+}
+
 int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                          void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
   if (int rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s)) return rc;
   return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, rec_off);
 }
 
-// Pipeline over nblocks.  Default: one stream.  With CU partitioning (cu_split >
-// 0, not while profiling), the batch is cut into chunks; RS of every chunk runs
-// on rs_stream (its own CUs), the commitment of chunk i on sha_stream (the other
-// CUs) after RS(i) -- so RS(i+1) overlaps commit(i).  Otherwise, with nsub > 1,
-// chunks go to independent sub-streams.
+// Pipeline over nblocks on `s`; with nsub > 1 (CDA_STREAMS) independent chunks of
+// blocks go to sub-streams forked from / joined back into `s` (serial while
+// profiling so per-kernel event timings do not overlap).  Measured on MI355X:
+// one stream is as fast or faster (each kernel already fills the GPU), and
+// CU-masked streams (RS on some CUs, SHA on the rest) were 2-5x slower.
 int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                      void* d_dah, unsigned long long* d_status, hipStream_t s) {
   const uint32_t w = 2 * k;
@@ -240,32 +304,8 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (rc) return rc;
   rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
   if (rc) return rc;
-  if (c->rs_stream && !c->prof && nblocks > 1) {
-    const int nch = (int)std::min<uint32_t>((uint32_t)c->pipe_chunks, nblocks);
-    if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
-        !dev_ok(c, hipStreamWaitEvent(c->rs_stream, c->fork_ev, 0), "hipStreamWaitEvent") ||
-        !dev_ok(c, hipStreamWaitEvent(c->sha_stream, c->fork_ev, 0), "hipStreamWaitEvent"))
-      return CDA_E_DEVICE;
-    uint32_t done = 0;
-    for (int i = 0; i < nch; i++) {
-      const uint32_t nb = (nblocks - done) / (uint32_t)(nch - i);
-      if ((rc = enqueue_rs(c, k, nb, d_ods + (size_t)done * k * k * CDA_SHARE, d_eds + (size_t)done * w * w * CDA_SHARE,
-                           c->rs_stream)))
-        return rc;
-      if (!dev_ok(c, hipEventRecord(c->rs_ev[i], c->rs_stream), "hipEventRecord") ||
-          !dev_ok(c, hipStreamWaitEvent(c->sha_stream, c->rs_ev[i], 0), "hipStreamWaitEvent"))
-        return CDA_E_DEVICE;
-      if ((rc = enqueue_commit(c, k, nb, d_eds + (size_t)done * w * w * CDA_SHARE,
-                               (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES, (uint8_t*)d_dah + (size_t)done * 32,
-                               d_status + done, c->sha_stream, (size_t)done * w * w)))
-        return rc;
-      done += nb;
-    }
-    if (!dev_ok(c, hipEventRecord(c->join_ev[0], c->sha_stream), "hipEventRecord") ||
-        !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[0], 0), "hipStreamWaitEvent"))
-      return CDA_E_DEVICE;
-    return CDA_OK;
-  }
+  if (k == 128 && c->fused && nblocks >= 2)
+    return enqueue_pipeline_fused(c, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s);
   const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
   if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
   if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
@@ -325,28 +365,12 @@ int cda_init(int device, cda_ctx** out) {
     return CDA_E_DEVICE;
   }
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
-  if (const char* e = getenv("CDA_CU_SPLIT")) c->cu_split = std::max(0, atoi(e));
-  if (const char* e = getenv("CDA_PIPE_CHUNKS")) c->pipe_chunks = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
+  if (const char* e = getenv("CDA_FUSED")) c->fused = atoi(e) != 0;
+  if (const char* e = getenv("CDA_CHUNKS")) c->chunks = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
     ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&c->rs_ev[i], hipEventDisableTiming) == hipSuccess;
-  if (ok && c->cu_split > 0) {
-    int ncu = 0;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    if (ncu > 0 && c->cu_split < ncu) {
-      // spread each partition evenly over the CU numbering (and so over the XCDs)
-      std::vector<uint32_t> rs_mask((ncu + 31) / 32, 0u), sha_mask((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; i++) {
-        const bool rs = (long long)(i + 1) * c->cu_split / ncu > (long long)i * c->cu_split / ncu;
-        (rs ? rs_mask : sha_mask)[i / 32] |= 1u << (i % 32);
-      }
-      ok = hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()) == hipSuccess &&
-           hipExtStreamCreateWithCUMask(&c->sha_stream, (uint32_t)sha_mask.size(), sha_mask.data()) == hipSuccess;
-      if (!ok) fprintf(stderr, "cda_init: hipExtStreamCreateWithCUMask failed\n");
-    }
-  }
+         hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     delete c;
     return CDA_E_DEVICE;
@@ -368,10 +392,7 @@ void cda_free(cda_ctx* c) {
     for (int i = 0; i < cda_ctx::kMaxSub; i++) {
       if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
-      if (c->rs_ev[i]) (void)hipEventDestroy(c->rs_ev[i]);
     }
-    if (c->rs_stream) (void)hipStreamDestroy(c->rs_stream);
-    if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     (void)hipStreamDestroy(c->stream);
   }

@@ -1,0 +1,158 @@
+// nmt_dev.h — erasured-NMT leaf hashing device code shared by nmt_kernels.hip
+// (leaf_hash_kernel) and rs_kernels.hip (the fused RS + leaf kernel).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cda_internal.h"
+#include "sha256_dev.h"
+
+namespace cda {
+
+// ---------------------------------------------------------------------------
+// Leaf hashing: one thread per EDS cell.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load16(const uint4* p, uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint4 v = p[i];
+    w[4 * i + 0] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+
+// Big-endian namespace words of a 29-byte namespace held little-endian in n[0..7]
+// (n[7] byte 0 = ns[28]) compared lexicographically: returns -1/0/1.
+__device__ __forceinline__ int ns_cmp(const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t x = bswap(a[i]), y = bswap(b[i]);
+    if (i == 7) {
+      x >>= 24;
+      y >>= 24;
+    }
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return 0;
+}
+
+// Leaf record of one 512-B share whose first 64 bytes are already in A[0..16):
+// ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share) ‖ 6 zero bytes, ns = share[0:29] if q0 else 0xFF×29.
+__device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q0, uint4* out) {
+  uint32_t ns[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ns[i] = q0 ? A[i] : 0xFFFFFFFFu;
+  uint32_t st[8];
+  sha256_init(st);
+  uint32_t m[16];
+  // block 0: 0x00 ‖ ns[0..29) ‖ share[0..34)
+  if (q0) {
+    m[0] = be_window(0u, A[0], 3);
+#pragma unroll
+    for (int i = 1; i < 7; i++) m[i] = be_window(A[i - 1], A[i], 3);
+    // bytes 28..31 = ns[27], ns[28], share[0], share[1]
+    m[7] = (be_window(A[6], A[7], 3) & 0xFFFF0000u) | (bswap(A[0]) >> 16);
+  } else {
+    m[0] = 0x00FFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 7; i++) m[i] = 0xFFFFFFFFu;
+    m[7] = 0xFFFF0000u | (bswap(A[0]) >> 16);
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) m[i] = be_window(A[i - 8], A[i - 7], 2);
+  sha256_compress(st, m);
+  // blocks 1..7: message words 16j..16j+15 = share bytes 64j-30.. : windows of S[16j-8 .. 16j+8].
+  // H carries the upper half of the previous 16-word chunk.
+  uint32_t H[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) H[i] = A[8 + i];
+#pragma unroll
+  for (int j = 1; j < 8; j++) {
+    uint32_t C[16];
+    load16(sh + 4 * j, C);
+#pragma unroll
+    for (int i = 0; i < 7; i++) m[i] = be_window(H[i], H[i + 1], 2);
+    m[7] = be_window(H[7], C[0], 2);
+#pragma unroll
+    for (int i = 8; i < 16; i++) m[i] = be_window(C[i - 8], C[i - 7], 2);
+    sha256_compress(st, m);
+#pragma unroll
+    for (int i = 0; i < 8; i++) H[i] = C[8 + i];
+  }
+  // block 8: share bytes 482..511, 0x80, zeros, bit length 542*8
+#pragma unroll
+  for (int i = 0; i < 7; i++) m[i] = be_window(H[i], H[i + 1], 2);
+  m[7] = be_window(H[7], 0x80u, 2);
+#pragma unroll
+  for (int i = 8; i < 15; i++) m[i] = 0;
+  m[15] = 542u * 8u;
+  sha256_compress(st, m);
+  // record: ns ‖ ns ‖ digest ‖ 6 zero bytes
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = bswap(st[i]);
+  uint32_t o[24];
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = ns[i];
+  o[7] = (ns[7] & 0xFFu) | (ns[0] << 8);
+#pragma unroll
+  for (int i = 8; i < 14; i++) o[i] = le_window(ns[i - 8], ns[i - 7], 3);
+  o[14] = (le_window(ns[6], ns[7], 3) & 0xFFFFu) | (d[0] << 16);
+#pragma unroll
+  for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
+  o[22] = d[7] >> 16;
+  o[23] = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) out[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
+
+// One EDS cell `gid` (= blk * w^2 + r * w + c) of a batch: push-order check against
+// its Q0 right / lower neighbours, then its 96-B leaf record.
+__device__ __forceinline__ void leaf_cell(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
+                                          unsigned long long* __restrict__ status, int k, int log2w, uint32_t gid) {
+  const int w = 1 << log2w;
+  const uint32_t cell = gid & ((1u << (2 * log2w)) - 1);
+  const uint32_t blk = gid >> (2 * log2w);
+  const int r = (int)(cell >> log2w), c = (int)(cell & (w - 1));
+  const bool q0 = (r < k) && (c < k);
+  const uint4* sh = reinterpret_cast<const uint4*>(eds + (size_t)gid * CDA_SHARE);
+
+  uint32_t A[16];
+  load16(sh, A);
+  uint32_t ns[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ns[i] = A[i];
+
+  // Namespace order (nmt Push ErrInvalidPushOrder) — checked for Q0 neighbours;
+  // parity leaves carry 0xFF×29, the maximum, so only Q0 pairs can violate it.
+  if (q0) {
+    if (c + 1 < k) {
+      uint32_t nb[8];
+      const uint4* p = reinterpret_cast<const uint4*>(eds + ((size_t)gid + 1) * CDA_SHARE);
+      uint4 v0 = p[0], v1 = p[1];
+      nb[0] = v0.x; nb[1] = v0.y; nb[2] = v0.z; nb[3] = v0.w;
+      nb[4] = v1.x; nb[5] = v1.y; nb[6] = v1.z; nb[7] = v1.w;
+      if (ns_cmp(nb, ns) < 0) {
+        unsigned long long key = ((unsigned long long)CDA_AXIS_ROW << 40) | ((unsigned long long)r << 20) | (c + 1);
+        atomicMin(status + blk, key);
+      }
+    }
+    if (r + 1 < k) {
+      uint32_t nb[8];
+      const uint4* p = reinterpret_cast<const uint4*>(eds + ((size_t)gid + w) * CDA_SHARE);
+      uint4 v0 = p[0], v1 = p[1];
+      nb[0] = v0.x; nb[1] = v0.y; nb[2] = v0.z; nb[3] = v0.w;
+      nb[4] = v1.x; nb[5] = v1.y; nb[6] = v1.z; nb[7] = v1.w;
+      if (ns_cmp(nb, ns) < 0) {
+        unsigned long long key = ((unsigned long long)CDA_AXIS_COL << 40) | ((unsigned long long)c << 20) | (r + 1);
+        atomicMin(status + blk, key);
+      }
+    }
+  }
+
+  leaf_record(sh, A, q0, nodes + (size_t)gid * 6);
+}
+
+}  // namespace cda

@@ -25,6 +25,8 @@
 #include <vector>
 
 #include "cda_internal.h"
+#include "gf8_mul_asm.h"
+#include "nmt_dev.h"
 
 namespace cda {
 
@@ -206,30 +208,9 @@ __device__ __forceinline__ void apply8(uint32_t (&v)[8], const uint8_t (&cols)[8
   for (int i = 0; i < 8; i++) v[i] = o[i];
 }
 
-// X ^= c * Y in the standard basis; c is wave-uniform.
-__device__ __forceinline__ void gf8_muladd_poly(uint32_t (&X)[8], const uint32_t (&Y)[8], unsigned c) {
-  uint32_t T[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) T[j] = Y[j];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    if (c & (1u << i)) {
-#pragma unroll
-      for (int j = 0; j < 8; j++) X[j] ^= T[j];
-    }
-    if (i < 7) {  // T *= alpha; unconditional so T's registers are renamed statically
-      const uint32_t t = T[7];
-      T[7] = T[6];
-      T[6] = T[5];
-      T[5] = T[4];
-      T[4] = T[3] ^ t;
-      T[3] = T[2] ^ t;
-      T[2] = T[1] ^ t;
-      T[1] = T[0];
-      T[0] = t;
-    }
-  }
-}
+// X ^= c * Y in the standard basis (c wave-uniform): gf8_muladd_asm, generated by
+// tools/gen_gf8_asm.py -- 21 v_xor for alpha^i * Y plus one v_xor / v_bitop3 XOR3 per
+// plane for each non-zero pair of bits of c.
 
 template <bool INVERSE>
 __device__ __forceinline__ void bfly_p(uint32_t (&X)[8], uint32_t (&Y)[8], unsigned c) {
@@ -237,7 +218,7 @@ __device__ __forceinline__ void bfly_p(uint32_t (&X)[8], uint32_t (&Y)[8], unsig
 #pragma unroll
     for (int j = 0; j < 8; j++) Y[j] ^= X[j];
   }
-  if (c != 0u) gf8_muladd_poly(X, Y, c);
+  if (c != 0u) gf8_muladd_asm(X, Y, c);
   if (!INVERSE) {
 #pragma unroll
     for (int j = 0; j < 8; j++) Y[j] ^= X[j];
@@ -288,32 +269,26 @@ __device__ __forceinline__ void layer2_u(uint32_t (&E)[8][8], int w, int f, int 
 }
 
 // d = 0 across lane halves (element x in lanes 0..31, x+1 in lanes 32..63).
+// v_permlane32_swap(a, a) hands every lane both x (lanes 0..31's a) and y (lanes
+// 32..63's a); both halves compute the butterfly, and a second swap puts x' back
+// in the low half and y' in the high half.  No LDS, no lane selects.
 template <bool INVERSE, int M>
 __device__ __forceinline__ void layer2_d0(uint32_t (&E)[8][8], int w, int f, bool upper) {
+  (void)upper;
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int x = x2_of(w, 0, r, f);
     const unsigned c = c_cpoly8[INVERSE ? (M - 1 + x + 1) : x];
-    uint32_t P[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) P[j] = __shfl_xor(E[r][j], 32);
     uint32_t X[8], Y[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      X[j] = upper ? P[j] : E[r][j];
-      Y[j] = upper ? E[r][j] : P[j];
+      const auto p = __builtin_amdgcn_permlane32_swap(E[r][j], E[r][j], false, false);
+      X[j] = p[0];
+      Y[j] = p[1];
     }
-    if (INVERSE) {  // y' = x ^ y ; x' = x ^ c*y'
+    bfly_p<INVERSE>(X, Y, c);
 #pragma unroll
-      for (int j = 0; j < 8; j++) Y[j] ^= X[j];
-      if (c != 0u) gf8_muladd_poly(X, Y, c);
-    } else {  // x' = x ^ c*y ; y' = y ^ x'
-      if (c != 0u) gf8_muladd_poly(X, Y, c);
-#pragma unroll
-      for (int j = 0; j < 8; j++) Y[j] ^= X[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) E[r][j] = upper ? Y[j] : X[j];
+    for (int j = 0; j < 8; j++) E[r][j] = __builtin_amdgcn_permlane32_swap(X[j], Y[j], false, false)[0];
   }
 }
 
@@ -342,16 +317,15 @@ __device__ __forceinline__ void exchange2(uint32_t (&E)[8][8], uint4* xbuf, int 
   }
 }
 
+// Work of workgroup `wg` (blockDim = 64 << (L - 4)); xbuf = [M][32] x 16 B LDS (L > 4).
 template <int L>
-__global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegArgs a) {
+__device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* xbuf) {
   constexpr int M = 1 << L;
   constexpr int NW = 1 << (L - 4);
-  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];  // [M][32] x 16 B (L > 4 only)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & (NW - 1);
   const int u = lane & 15, cwi = (lane >> 4) & 1, sw = lane >> 5, li = lane & 31;
   const bool upper = sw != 0;
-  int wg = blockIdx.x;
   const int slice = wg % a.slices;
   wg /= a.slices;
   const int grp = wg % a.groups_per_blk;
@@ -415,6 +389,47 @@ __global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegA
   }
 }
 
+template <int L>
+__global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
+  rs_g2_body<L>(a, blockIdx.x, xbuf);
+}
+
+// ===========================================================================
+// Fused RS + leaf kernel (k = 128 block pipeline).  One launch carries three
+// independent pieces of the software pipeline over chunks of blocks: row encode
+// of chunk t, column encode of chunk t-1 and leaf hashing of chunk t-2.  Their
+// workgroups are interleaved over blockIdx so every CU holds a mix: the RS
+// workgroups' HBM phases overlap the leaf workgroups' SHA-256 VALU work (with
+// separate launches each RS launch alternates HBM-bound and VALU-bound phases
+// in lockstep).  All roles use 512 threads and the RS LDS footprint.
+// ===========================================================================
+struct FusedArgs {
+  Rs8RegArgs rows, cols;
+  int rows_wgs, cols_wgs, leaf_wgs;
+  const uint8_t* leaf_eds;
+  uint4* leaf_nodes;
+  unsigned long long* leaf_status;
+  uint32_t leaf_cells;
+};
+
+__global__ void __launch_bounds__(512, 4) fused_rs_leaf_kernel(FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
+  const uint32_t b = blockIdx.x, total = gridDim.x;
+  const uint32_t nrs = (uint32_t)(a.rows_wgs + a.cols_wgs);
+  // Bresenham interleave: RS workgroups spread evenly through the grid
+  const uint32_t rs_before = (uint32_t)(((unsigned long long)b * nrs) / total);
+  const uint32_t rs_after = (uint32_t)(((unsigned long long)(b + 1) * nrs) / total);
+  if (rs_after > rs_before) {
+    const int j = (int)rs_before;
+    const bool col = j < a.cols_wgs;
+    rs_g2_body<7>(col ? a.cols : a.rows, col ? j : j - a.cols_wgs, xbuf);
+  } else {
+    const uint32_t gid = (b - rs_before) * 512u + threadIdx.x;
+    if (gid < a.leaf_cells) leaf_cell(a.leaf_eds, a.leaf_nodes, a.leaf_status, 128, 8, gid);
+  }
+}
+
 int rs_init_device_tables(int device) {
   (void)device;
   const LeoTables& t = leo_tables(8);
@@ -443,6 +458,9 @@ int rs_init_device_tables(int device) {
                         (const void*)rs_encode8_g2_kernel<6>, (const void*)rs_encode8_g2_kernel<7>};
   for (auto f : g2k)
     if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) != hipSuccess) return -1;
+  if (hipFuncSetAttribute((const void*)fused_rs_leaf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) !=
+      hipSuccess)
+    return -1;
   return 0;
 }
 
@@ -452,27 +470,56 @@ static int ilog2(int v) {
   return l;
 }
 
+static Rs8RegArgs reg_args(const RsJob& j) {
+  Rs8RegArgs r{};
+  r.src = j.src;
+  r.src_blk = j.src_blk;
+  r.src_cw = j.src_cw;
+  r.src_sh = j.src_sh;
+  r.dst = j.dst;
+  r.dst_blk = j.dst_blk;
+  r.dst_cw = j.dst_cw;
+  r.dst_sh = j.dst_sh;
+  r.cpy = j.cpy;
+  r.cpy_blk = j.cpy_blk;
+  r.cpy_cw = j.cpy_cw;
+  r.cpy_sh = j.cpy_sh;
+  r.k = j.k;
+  r.groups_per_blk = j.cw_per_blk / 2;
+  r.slices = j.shard_len / 512;
+  return r;
+}
+
+int launch_fused_rs_leaf(const RsJob* rows, const RsJob* cols, const uint8_t* leaf_eds, void* leaf_nodes,
+                         unsigned long long* leaf_status, int leaf_blocks, hipStream_t s) {
+  FusedArgs f{};
+  for (const RsJob* j : {rows, cols})
+    if (j && (j->k != 128 || j->cw_per_blk % 2 || j->shard_len != 512)) return -2;
+  if (rows) {
+    f.rows = reg_args(*rows);
+    f.rows_wgs = rows->nblk * f.rows.groups_per_blk;
+  }
+  if (cols) {
+    f.cols = reg_args(*cols);
+    f.cols_wgs = cols->nblk * f.cols.groups_per_blk;
+  }
+  f.leaf_eds = leaf_eds;
+  f.leaf_nodes = (uint4*)leaf_nodes;
+  f.leaf_status = leaf_status;
+  f.leaf_cells = (uint32_t)leaf_blocks * 256u * 256u;
+  f.leaf_wgs = (int)(f.leaf_cells / 512u);
+  const unsigned grid = (unsigned)(f.rows_wgs + f.cols_wgs + f.leaf_wgs);
+  if (grid == 0) return 0;
+  hipLaunchKernelGGL(fused_rs_leaf_kernel, dim3(grid), dim3(512), 128 * 32 * 16, s, f);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   if (j.k < 1 || j.k > 128 || j.shard_len % 64 != 0) return -2;
   const int L = ilog2(j.k);
   // Batched path: 2 codewords per workgroup, register-resident (k >= 16).
   if (L >= 4 && j.cw_per_blk % 2 == 0 && j.shard_len % 512 == 0) {
-    Rs8RegArgs r{};
-    r.src = j.src;
-    r.src_blk = j.src_blk;
-    r.src_cw = j.src_cw;
-    r.src_sh = j.src_sh;
-    r.dst = j.dst;
-    r.dst_blk = j.dst_blk;
-    r.dst_cw = j.dst_cw;
-    r.dst_sh = j.dst_sh;
-    r.cpy = j.cpy;
-    r.cpy_blk = j.cpy_blk;
-    r.cpy_cw = j.cpy_cw;
-    r.cpy_sh = j.cpy_sh;
-    r.k = j.k;
-    r.groups_per_blk = j.cw_per_blk / 2;
-    r.slices = j.shard_len / 512;
+    const Rs8RegArgs r = reg_args(j);
     const long long grid = (long long)j.nblk * r.groups_per_blk * r.slices;
     if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
     const size_t lds = L > 4 ? (size_t)(1 << L) * 32 * 16 : 0;

@@ -64,6 +64,39 @@ def test_batch_matches_single(ctx):
         assert dah[b].tobytes() == dah_o
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("chunks", ["4", "3"])
+def test_batch_k128_pipeline(fused, chunks, monkeypatch):
+    """k=128 batches run the fused RS+leaf software pipeline (uneven chunks) or the plain one."""
+    import cda
+    monkeypatch.setenv("CDA_FUSED", fused)
+    monkeypatch.setenv("CDA_CHUNKS", chunks)
+    c = cda.Context(0)
+    try:
+        k, nb = 128, 7
+        ods = np.stack([O.gen_ods(k, 0xBEEF + b) for b in range(nb)])
+        eds, rr, cr, dah = c.extend_commit_batch(ods)
+        for b in range(nb):
+            rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods[b])
+            assert np.array_equal(eds[b], eds_o), f"block {b} EDS differs"
+            assert np.array_equal(rr[b], rr_o) and np.array_equal(cr[b], cr_o), f"block {b} roots differ"
+            assert dah[b].tobytes() == dah_o
+    finally:
+        c.close()
+
+
+def test_batch_k128_push_error_block(ctx):
+    """A push-order error in one block of a fused-pipeline batch names that block, axis, index and leaf."""
+    from cda import CdaError
+    k, nb = 128, 5
+    ods = np.stack([O.gen_ods(k, 0xFACE + b) for b in range(nb)])
+    ods[3, [130, 131]] = ods[3, [131, 130]]  # row 1 leaves 2 and 3 swapped
+    with pytest.raises(CdaError) as ei:
+        ctx.extend_commit_batch(ods)
+    e = ei.value
+    assert (e.code, e.block, e.axis, e.index, e.leaf) == (-5, 3, 0, 1, 3)
+
+
 def test_random_bytes_not_sorted_rows_are_rejected(ctx):
     from cda import CdaError
     k = 8
