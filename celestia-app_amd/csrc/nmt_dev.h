@@ -40,6 +40,9 @@ __device__ __forceinline__ int ns_cmp(const uint32_t* a, const uint32_t* b) {
 
 // Leaf record of one 512-B share whose first 64 bytes are already in A[0..16):
 // ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share) ‖ 6 zero bytes, ns = share[0:29] if q0 else 0xFF×29.
+// COMPACT keeps blocks 1..7 as a loop (one copy of the compression code) for
+// kernels whose instruction footprint matters (the fused RS + leaf kernel).
+template <bool COMPACT = false>
 __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q0, uint4* out) {
   uint32_t ns[8];
 #pragma unroll
@@ -68,7 +71,7 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
   uint32_t H[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) H[i] = A[8 + i];
-#pragma unroll
+#pragma unroll(COMPACT ? 1 : 7)
   for (int j = 1; j < 8; j++) {
     uint32_t C[16];
     load16(sh + 4 * j, C);
@@ -110,6 +113,7 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
 
 // One EDS cell `gid` (= blk * w^2 + r * w + c) of a batch: push-order check against
 // its Q0 right / lower neighbours, then its 96-B leaf record.
+template <bool COMPACT = false>
 __device__ __forceinline__ void leaf_cell(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
                                           unsigned long long* __restrict__ status, int k, int log2w, uint32_t gid) {
   const int w = 1 << log2w;
@@ -152,7 +156,7 @@ __device__ __forceinline__ void leaf_cell(const uint8_t* __restrict__ eds, uint4
     }
   }
 
-  leaf_record(sh, A, q0, nodes + (size_t)gid * 6);
+  leaf_record<COMPACT>(sh, A, q0, nodes + (size_t)gid * 6);
 }
 
 }  // namespace cda

@@ -426,7 +426,7 @@ __global__ void __launch_bounds__(512, 4) fused_rs_leaf_kernel(FusedArgs a) {
     rs_g2_body<7>(col ? a.cols : a.rows, col ? j : j - a.cols_wgs, xbuf);
   } else {
     const uint32_t gid = (b - rs_before) * 512u + threadIdx.x;
-    if (gid < a.leaf_cells) leaf_cell(a.leaf_eds, a.leaf_nodes, a.leaf_status, 128, 8, gid);
+    if (gid < a.leaf_cells) leaf_cell<true>(a.leaf_eds, a.leaf_nodes, a.leaf_status, 128, 8, gid);
   }
 }
 

@@ -64,6 +64,28 @@ def test_batch_matches_single(ctx):
         assert dah[b].tobytes() == dah_o
 
 
+def test_mainnet_block_408_data_hash(ctx):
+    """Real block (reference fixture x/blob/test/testdata/block_response.json): GPU DAH == header data_hash."""
+    import os
+    from cda import da
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mainnet_h408.npz"))
+    ods, want = z["ods"], z["data_hash"].tobytes()
+    eds, rr, cr, dah = ctx.extend_commit(ods)
+    assert dah == want
+    rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods)
+    assert np.array_equal(eds, eds_o) and np.array_equal(rr, rr_o) and np.array_equal(cr, cr_o)
+    h = da.new_data_availability_header(da.extend_shares([bytes(s) for s in ods]))
+    assert h.hash() == want
+    # Repair from Q0 only reproduces the block's EDS
+    w = 64
+    present = np.zeros(w * w, np.uint8)
+    present.reshape(w, w)[:32, :32] = 1
+    damaged = eds.copy()
+    damaged[present == 0] = 0
+    out, pres = ctx.repair(damaged, present, rr, cr)
+    assert np.array_equal(out, eds) and pres.all()
+
+
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("chunks", ["4", "3"])
 def test_batch_k128_pipeline(fused, chunks, monkeypatch):

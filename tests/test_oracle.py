@@ -186,3 +186,22 @@ def test_bench_generator_matches_oracle_generator():
     spec.loader.exec_module(bench)
     for k in (1, 4, 16):
         assert np.array_equal(bench.gen_ods(k, 0xC0FFEE + k), O.gen_ods(k, 0xC0FFEE + k))
+
+
+# ---- real-data pin: Celestia mainnet block 408 (reference fixture) -------------------------
+def _mainnet():
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mainnet_h408.npz")
+    z = np.load(p)  # allow_pickle=False (default): plain arrays written by tests/golden/make_mainnet_block.py
+    return z["ods"], z["data_hash"].tobytes()
+
+
+def test_oracle_reproduces_mainnet_block_408_data_hash():
+    """ODS built from x/blob/test/testdata/block_response.json; its data_hash pins Leopard FF8 + NMT + DAH."""
+    ods, want = _mainnet()
+    assert ods.shape == (1024, 512)
+    rc, eds, rr, cr, dah = O.extend_commit(ods)
+    assert rc == 0 and dah == want
+    # non-constant data: parity differs from the data it encodes
+    e = eds.reshape(64, 64, 512)
+    assert not np.array_equal(e[:32, 32:], e[:32, :32])
