@@ -43,8 +43,6 @@ def kernel_step_bytes(name, k, B):
     NMT levels: read 2 child nodes, write 1 (90 B each); dah: read 4k roots.
     """
     w, S, N = 2 * k, 512, 90
-    if name == "fused_rs_leaf":  # rows + cols + leaf hashing in one software-pipelined kernel
-        return sum(kernel_step_bytes(n, k, B) for n in ("x_rows", "x_cols", "leaf_hash"))
     if name.endswith("_rows"):
         return B * 3 * k * k * S
     if name.endswith("_cols"):
@@ -245,7 +243,7 @@ def main():
     # ceiling = register-only sha256_compress throughput measured by tools/sha_ubench.hip.
     comp_per_s = block_compressions_engine(k) * value / world
     SHA_CEIL = 28.6e9
-    sha_kernels = [n for n in kern if n in ("leaf_hash", "nmt_level1", "nmt_level", "fused_rs_leaf")]
+    sha_kernels = [n for n in kern if n in ("leaf_hash", "nmt_level1", "nmt_level")]
     sha_ms = sum(kern[n]["total_ms"] for n in sha_kernels) / prof_steps
     sha_comp_step = B * (block_compressions_engine(k) - 2 * (2 * (2 * k)) + 2)  # minus the DAH's
     sha_rate = sha_comp_step / (sha_ms * 1e-3) if sha_ms else None

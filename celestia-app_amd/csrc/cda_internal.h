@@ -52,10 +52,6 @@ int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d
                      int ncw, int k, int shard_len, hipStream_t s);
 int launch_rs_encode8(const RsJob& job, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
-// One launch of the k = 128 software pipeline: rows job, cols job (either may be
-// null) and leaf hashing of `leaf_blocks` blocks starting at leaf_eds.
-int launch_fused_rs_leaf(const RsJob* rows, const RsJob* cols, const uint8_t* leaf_eds, void* leaf_nodes,
-                         unsigned long long* leaf_status, int leaf_blocks, hipStream_t s);
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
                      hipStream_t s);
 int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int nblocks, int level, hipStream_t s);

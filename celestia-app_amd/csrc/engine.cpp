@@ -34,8 +34,6 @@ struct cda_ctx {
   // another's hashing (no dependency between blocks).
   static constexpr int kMaxSub = 8;
   int nsub = 1;
-  // fused k = 128 pipeline (CDA_FUSED=0 disables) over `chunks` chunks (CDA_CHUNKS)
-  int fused = 1, chunks = 4;
   hipStream_t sub[kMaxSub] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::string last_err;
@@ -233,58 +231,6 @@ int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ed
   return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, rec_off);
 }
 
-// k = 128 software pipeline over chunks of blocks: launch t runs rows(chunk t),
-// cols(chunk t-1) and leaf hashing (chunk t-2) in one fused kernel; the NMT
-// levels + DAH of a chunk follow on sub-stream 0 once its leaves are done, so
-// they overlap the next fused launch.
-int enqueue_pipeline_fused(cda_ctx* c, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
-                           void* d_dah, unsigned long long* d_status, hipStream_t s) {
-  const uint32_t k = 128, w = 256;
-  const int nch = (int)std::min<uint32_t>((uint32_t)c->chunks, nblocks);
-  uint32_t first[cda_ctx::kMaxSub + 1];
-  for (int i = 0; i <= nch; i++) first[i] = (uint32_t)((unsigned long long)nblocks * i / nch);
-  auto nb = [&](int i) { return first[i + 1] - first[i]; };
-  auto ods = [&](int i) { return d_ods + (size_t)first[i] * k * k * CDA_SHARE; };
-  auto eds = [&](int i) { return d_eds + (size_t)first[i] * w * w * CDA_SHARE; };
-  hipStream_t t_s = c->prof ? s : c->sub[0];
-  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
-  if (t_s != s && (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
-                   !dev_ok(c, hipStreamWaitEvent(t_s, c->fork_ev, 0), "hipStreamWaitEvent")))
-    return CDA_E_DEVICE;
-  for (int t = 0; t < nch + 2; t++) {
-    RsJob rj, cj;
-    const RsJob* rp = nullptr;
-    const RsJob* cp = nullptr;
-    if (t < nch) {
-      rj = rows_job(k, nb(t), ods(t), eds(t));
-      rp = &rj;
-    }
-    if (t >= 1 && t - 1 < nch) {
-      cj = cols_job(k, nb(t - 1), eds(t - 1));
-      cp = &cj;
-    }
-    const int lc = t - 2;
-    {
-      ProfScope ps(c, "fused_rs_leaf", s);
-      const int lr = launch_fused_rs_leaf(rp, cp, lc >= 0 ? eds(lc) : nullptr,
-                                          lc >= 0 ? bufs0(c, (size_t)first[lc] * w * w) : nullptr,
-                                          lc >= 0 ? d_status + first[lc] : nullptr, lc >= 0 ? (int)nb(lc) : 0, s);
-      if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
-    }
-    if (lc < 0) continue;
-    if (t_s != s && (!dev_ok(c, hipEventRecord(c->join_ev[lc % cda_ctx::kMaxSub], s), "hipEventRecord") ||
-                     !dev_ok(c, hipStreamWaitEvent(t_s, c->join_ev[lc % cda_ctx::kMaxSub], 0), "hipStreamWaitEvent")))
-      return CDA_E_DEVICE;
-    if (int rc = enqueue_trees(c, k, nb(lc), (uint8_t*)d_roots + (size_t)first[lc] * 2 * w * CDA_REC_BYTES,
-                               (uint8_t*)d_dah + (size_t)first[lc] * 32, t_s, (size_t)first[lc] * w * w))
-      return rc;
-  }
-  if (t_s != s && (!dev_ok(c, hipEventRecord(c->fork_ev, t_s), "hipEventRecord") ||
-                   !dev_ok(c, hipStreamWaitEvent(s, c->fork_ev, 0), "hipStreamWaitEvent")))
-    return CDA_E_DEVICE;
-  return CDA_OK;
-}
-
 int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                          void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
   if (int rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s)) return rc;
@@ -304,8 +250,6 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (rc) return rc;
   rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
   if (rc) return rc;
-  if (k == 128 && c->fused && nblocks >= 2)
-    return enqueue_pipeline_fused(c, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s);
   const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
   if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
   if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
@@ -365,8 +309,6 @@ int cda_init(int device, cda_ctx** out) {
     return CDA_E_DEVICE;
   }
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
-  if (const char* e = getenv("CDA_FUSED")) c->fused = atoi(e) != 0;
-  if (const char* e = getenv("CDA_CHUNKS")) c->chunks = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
     ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&

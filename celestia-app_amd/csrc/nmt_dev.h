@@ -1,5 +1,5 @@
-// nmt_dev.h — erasured-NMT leaf hashing device code shared by nmt_kernels.hip
-// (leaf_hash_kernel) and rs_kernels.hip (the fused RS + leaf kernel).
+// nmt_dev.h — erasured-NMT leaf hashing device code (leaf_hash_kernel and the
+// single-tree / axis-list leaf kernels in nmt_kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -40,9 +40,8 @@ __device__ __forceinline__ int ns_cmp(const uint32_t* a, const uint32_t* b) {
 
 // Leaf record of one 512-B share whose first 64 bytes are already in A[0..16):
 // ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share) ‖ 6 zero bytes, ns = share[0:29] if q0 else 0xFF×29.
-// COMPACT keeps blocks 1..7 as a loop (one copy of the compression code) for
-// kernels whose instruction footprint matters (the fused RS + leaf kernel).
-template <bool COMPACT = false>
+// Blocks 1..7 stay a loop (one copy of the compression code: measured as fast as
+// the unrolled form on MI355X, with half the instruction footprint).
 __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q0, uint4* out) {
   uint32_t ns[8];
 #pragma unroll
@@ -71,7 +70,7 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
   uint32_t H[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) H[i] = A[8 + i];
-#pragma unroll(COMPACT ? 1 : 7)
+#pragma unroll 1
   for (int j = 1; j < 8; j++) {
     uint32_t C[16];
     load16(sh + 4 * j, C);
@@ -113,7 +112,6 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
 
 // One EDS cell `gid` (= blk * w^2 + r * w + c) of a batch: push-order check against
 // its Q0 right / lower neighbours, then its 96-B leaf record.
-template <bool COMPACT = false>
 __device__ __forceinline__ void leaf_cell(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
                                           unsigned long long* __restrict__ status, int k, int log2w, uint32_t gid) {
   const int w = 1 << log2w;
@@ -156,7 +154,7 @@ __device__ __forceinline__ void leaf_cell(const uint8_t* __restrict__ eds, uint4
     }
   }
 
-  leaf_record<COMPACT>(sh, A, q0, nodes + (size_t)gid * 6);
+  leaf_record(sh, A, q0, nodes + (size_t)gid * 6);
 }
 
 }  // namespace cda

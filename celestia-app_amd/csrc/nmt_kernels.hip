@@ -24,13 +24,12 @@
 
 namespace cda {
 
-template <bool COMPACT>
 __global__ void __launch_bounds__(256) leaf_hash_kernel(const uint8_t* __restrict__ eds, uint4* __restrict__ nodes,
                                                         unsigned long long* __restrict__ status, int k, int log2w,
                                                         uint32_t total_cells) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total_cells) return;
-  leaf_cell<COMPACT>(eds, nodes, status, k, log2w, gid);
+  leaf_cell(eds, nodes, status, k, log2w, gid);
 }
 
 // ---------------------------------------------------------------------------
@@ -296,13 +295,8 @@ int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long lon
   while ((1 << log2w) < w) log2w++;
   const uint32_t total = (uint32_t)nblocks * (uint32_t)w * (uint32_t)w;
   const uint32_t grid = (total + 255) / 256;
-  static const bool compact = getenv("CDA_LEAF_COMPACT") && atoi(getenv("CDA_LEAF_COMPACT")) != 0;
-  if (compact)
-    hipLaunchKernelGGL(leaf_hash_kernel<true>, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k,
-                       log2w, total);
-  else
-    hipLaunchKernelGGL(leaf_hash_kernel<false>, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k,
-                       log2w, total);
+  hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid), dim3(256), 0, s, d_eds, (uint4*)d_leaf_nodes, d_status, k,
+                     log2w, total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -26,7 +26,6 @@
 
 #include "cda_internal.h"
 #include "gf8_mul_asm.h"
-#include "nmt_dev.h"
 
 namespace cda {
 
@@ -395,41 +394,6 @@ __global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegA
   rs_g2_body<L>(a, blockIdx.x, xbuf);
 }
 
-// ===========================================================================
-// Fused RS + leaf kernel (k = 128 block pipeline).  One launch carries three
-// independent pieces of the software pipeline over chunks of blocks: row encode
-// of chunk t, column encode of chunk t-1 and leaf hashing of chunk t-2.  Their
-// workgroups are interleaved over blockIdx so every CU holds a mix: the RS
-// workgroups' HBM phases overlap the leaf workgroups' SHA-256 VALU work (with
-// separate launches each RS launch alternates HBM-bound and VALU-bound phases
-// in lockstep).  All roles use 512 threads and the RS LDS footprint.
-// ===========================================================================
-struct FusedArgs {
-  Rs8RegArgs rows, cols;
-  int rows_wgs, cols_wgs, leaf_wgs;
-  const uint8_t* leaf_eds;
-  uint4* leaf_nodes;
-  unsigned long long* leaf_status;
-  uint32_t leaf_cells;
-};
-
-__global__ void __launch_bounds__(512, 4) fused_rs_leaf_kernel(FusedArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
-  const uint32_t b = blockIdx.x, total = gridDim.x;
-  const uint32_t nrs = (uint32_t)(a.rows_wgs + a.cols_wgs);
-  // Bresenham interleave: RS workgroups spread evenly through the grid
-  const uint32_t rs_before = (uint32_t)(((unsigned long long)b * nrs) / total);
-  const uint32_t rs_after = (uint32_t)(((unsigned long long)(b + 1) * nrs) / total);
-  if (rs_after > rs_before) {
-    const int j = (int)rs_before;
-    const bool col = j < a.cols_wgs;
-    rs_g2_body<7>(col ? a.cols : a.rows, col ? j : j - a.cols_wgs, xbuf);
-  } else {
-    const uint32_t gid = (b - rs_before) * 512u + threadIdx.x;
-    if (gid < a.leaf_cells) leaf_cell<true>(a.leaf_eds, a.leaf_nodes, a.leaf_status, 128, 8, gid);
-  }
-}
-
 int rs_init_device_tables(int device) {
   (void)device;
   const LeoTables& t = leo_tables(8);
@@ -458,9 +422,7 @@ int rs_init_device_tables(int device) {
                         (const void*)rs_encode8_g2_kernel<6>, (const void*)rs_encode8_g2_kernel<7>};
   for (auto f : g2k)
     if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) != hipSuccess) return -1;
-  if (hipFuncSetAttribute((const void*)fused_rs_leaf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) !=
-      hipSuccess)
-    return -1;
+
   return 0;
 }
 
@@ -488,30 +450,6 @@ static Rs8RegArgs reg_args(const RsJob& j) {
   r.groups_per_blk = j.cw_per_blk / 2;
   r.slices = j.shard_len / 512;
   return r;
-}
-
-int launch_fused_rs_leaf(const RsJob* rows, const RsJob* cols, const uint8_t* leaf_eds, void* leaf_nodes,
-                         unsigned long long* leaf_status, int leaf_blocks, hipStream_t s) {
-  FusedArgs f{};
-  for (const RsJob* j : {rows, cols})
-    if (j && (j->k != 128 || j->cw_per_blk % 2 || j->shard_len != 512)) return -2;
-  if (rows) {
-    f.rows = reg_args(*rows);
-    f.rows_wgs = rows->nblk * f.rows.groups_per_blk;
-  }
-  if (cols) {
-    f.cols = reg_args(*cols);
-    f.cols_wgs = cols->nblk * f.cols.groups_per_blk;
-  }
-  f.leaf_eds = leaf_eds;
-  f.leaf_nodes = (uint4*)leaf_nodes;
-  f.leaf_status = leaf_status;
-  f.leaf_cells = (uint32_t)leaf_blocks * 256u * 256u;
-  f.leaf_wgs = (int)(f.leaf_cells / 512u);
-  const unsigned grid = (unsigned)(f.rows_wgs + f.cols_wgs + f.leaf_wgs);
-  if (grid == 0) return 0;
-  hipLaunchKernelGGL(fused_rs_leaf_kernel, dim3(grid), dim3(512), 128 * 32 * 16, s, f);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_rs_encode8(const RsJob& j, hipStream_t s) {

@@ -27,7 +27,15 @@ static const uint8_t kParityNs[ORA_NS] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0x
                                           0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
                                           0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF};
 
-void ora_sha256(const uint8_t* msg, size_t len, uint8_t out[32]) { SHA256(msg, len, out); }
+/* Low-level SHA256_* (SHA-NI block function, no per-call EVP algorithm fetch):
+ * OpenSSL 3's one-shot SHA256() fetches the digest under a global lock on every
+ * call, which made the threaded oracle slower than one thread. */
+void ora_sha256(const uint8_t* msg, size_t len, uint8_t out[32]) {
+  SHA256_CTX c;
+  SHA256_Init(&c);
+  if (len) SHA256_Update(&c, msg, len);
+  SHA256_Final(out, &c);
+}
 
 /* ------------------------------------------------------------------ */
 /* tiny parallel-for (rsmt2d fans out one goroutine per axis)          */

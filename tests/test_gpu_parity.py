@@ -86,13 +86,11 @@ def test_mainnet_block_408_data_hash(ctx):
     assert np.array_equal(out, eds) and pres.all()
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-@pytest.mark.parametrize("chunks", ["4", "3"])
-def test_batch_k128_pipeline(fused, chunks, monkeypatch):
-    """k=128 batches run the fused RS+leaf software pipeline (uneven chunks) or the plain one."""
+@pytest.mark.parametrize("streams", ["1", "3"])
+def test_batch_k128_pipeline(streams, monkeypatch):
+    """k=128 batches on one stream and split over 3 sub-streams (uneven chunks)."""
     import cda
-    monkeypatch.setenv("CDA_FUSED", fused)
-    monkeypatch.setenv("CDA_CHUNKS", chunks)
+    monkeypatch.setenv("CDA_STREAMS", streams)
     c = cda.Context(0)
     try:
         k, nb = 128, 7
@@ -108,7 +106,7 @@ def test_batch_k128_pipeline(fused, chunks, monkeypatch):
 
 
 def test_batch_k128_push_error_block(ctx):
-    """A push-order error in one block of a fused-pipeline batch names that block, axis, index and leaf."""
+    """A push-order error in one block of a batch names that block, axis, index and leaf."""
     from cda import CdaError
     k, nb = 128, 5
     ods = np.stack([O.gen_ods(k, 0xFACE + b) for b in range(nb)])
