@@ -188,7 +188,7 @@ __device__ __forceinline__ unsigned cpoly_of_log(const DecArgs& a, unsigned l) {
 
 template <int PL, bool INVERSE>
 __device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int log2D) {
-  const int U = a.U;
+  const int U = a.U, nU = a.n << a.log2U;
   const int nbu = (a.n >> 1) << a.log2U;
   for (int bu = threadIdx.x; bu < nbu; bu += blockDim.x) {
     const int p = bu >> a.log2U, u = bu & (U - 1);
@@ -199,8 +199,8 @@ __device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int
     uint32_t X[PL], Y[PL];
 #pragma unroll
     for (int j = 0; j < PL; j++) {
-      X[j] = st[(x * PL + j) * U + u];
-      Y[j] = st[(y * PL + j) * U + u];
+      X[j] = st[j * nU + x * U + u];
+      Y[j] = st[j * nU + y * U + u];
     }
     if (INVERSE) {
 #pragma unroll
@@ -213,8 +213,8 @@ __device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int
     }
 #pragma unroll
     for (int j = 0; j < PL; j++) {
-      st[(x * PL + j) * U + u] = X[j];
-      st[(y * PL + j) * U + u] = Y[j];
+      st[j * nU + x * U + u] = X[j];
+      st[j * nU + y * U + u] = Y[j];
     }
   }
   __syncthreads();
@@ -223,11 +223,11 @@ __device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int
 template <int PL>
 __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* st = smem;                                                        // [n][PL][U]
+  uint32_t* st = smem;  // [PL][n][U] plane-major: a wave's accesses within a plane are contiguous
   uint16_t* errl = reinterpret_cast<uint16_t*>(smem + (size_t)a.n * PL * a.U);  // [n]
   uint16_t* elist = errl + a.n;                                                // [n]
   __shared__ int ecount;
-  const int U = a.U;
+  const int U = a.U, nU = a.n << a.log2U;
   int wg = blockIdx.x;
   const int slice = wg % a.slices;
   const int cw = wg / a.slices;
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
       for (int j = 0; j < PL; j++) v[j] = 0;
     }
 #pragma unroll
-    for (int j = 0; j < PL; j++) st[(p * PL + j) * U + u] = v[j];
+    for (int j = 0; j < PL; j++) st[j * nU + p * U + u] = v[j];
   }
   __syncthreads();
   for (int lD = 0; lD < a.log2n; lD++) layer<PL, true>(st, a, 1 << lD, lD);
@@ -285,12 +285,12 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
       if (e < items) {
         const int x = e >> a.log2U, u = e & (U - 1);
 #pragma unroll
-        for (int j = 0; j < PL; j++) nv[it][j] = st[(x * PL + j) * U + u];
+        for (int j = 0; j < PL; j++) nv[it][j] = st[j * nU + x * U + u];
         for (int b = 0; b < a.log2n; b++) {
           if ((x >> b) & 1) continue;
           const int y = x + (1 << b);
 #pragma unroll
-          for (int j = 0; j < PL; j++) nv[it][j] ^= st[(y * PL + j) * U + u];
+          for (int j = 0; j < PL; j++) nv[it][j] ^= st[j * nU + y * U + u];
         }
       }
     }
@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
       if (e < items) {
         const int x = e >> a.log2U, u = e & (U - 1);
 #pragma unroll
-        for (int j = 0; j < PL; j++) st[(x * PL + j) * U + u] = nv[it][j];
+        for (int j = 0; j < PL; j++) st[j * nU + x * U + u] = nv[it][j];
       }
     }
     __syncthreads();
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
     if (shard < 0) continue;
     uint32_t w[PL], v[PL];
 #pragma unroll
-    for (int j = 0; j < PL; j++) w[j] = st[(p * PL + j) * U + u];
+    for (int j = 0; j < PL; j++) w[j] = st[j * nU + p * U + u];
     const unsigned l = (Field<PL>::kMod - errl[p]) % Field<PL>::kMod;
     mul_lane<PL>(v, w, cpoly_of_log<PL>(a, l));
     store_unit<PL>(base + shard * sstride + u * (PL * 4), v);

@@ -71,13 +71,13 @@ __device__ __forceinline__ void gf8_muladd(uint32_t x[8], const uint32_t y[8], u
 }
 
 template <bool INVERSE>
-__device__ __forceinline__ void butterfly8(uint32_t* st, int U, int x, int y, int u, unsigned log_m,
+__device__ __forceinline__ void butterfly8(uint32_t* st, int mU, int U, int x, int y, int u, unsigned log_m,
                                            unsigned long long cb) {
   uint32_t X[8], Y[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    X[j] = st[(x * 8 + j) * U + u];
-    Y[j] = st[(y * 8 + j) * U + u];
+    X[j] = st[j * mU + x * U + u];
+    Y[j] = st[j * mU + y * U + u];
   }
   if (INVERSE) {  // IFFT2
 #pragma unroll
@@ -90,8 +90,8 @@ __device__ __forceinline__ void butterfly8(uint32_t* st, int U, int x, int y, in
   }
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    st[(x * 8 + j) * U + u] = X[j];
-    st[(y * 8 + j) * U + u] = Y[j];
+    st[j * mU + x * U + u] = X[j];
+    st[j * mU + y * U + u] = Y[j];
   }
 }
 
@@ -107,10 +107,10 @@ __device__ __forceinline__ void rs_layer8(uint32_t* st, int m, int U, int log2U,
     if ((D << log2U) >= 64) {  // constant is wave-uniform: masks in SGPRs
       const int sidx = __builtin_amdgcn_readfirstlane(idx);
       const unsigned lm = c_skew8[sidx];
-      butterfly8<INVERSE>(st, U, x, y, u, lm, c_col8[lm]);
+      butterfly8<INVERSE>(st, m << log2U, U, x, y, u, lm, c_col8[lm]);
     } else {
       const unsigned lm = c_skew8[idx];
-      butterfly8<INVERSE>(st, U, x, y, u, lm, c_col8[lm]);
+      butterfly8<INVERSE>(st, m << log2U, U, x, y, u, lm, c_col8[lm]);
     }
   }
   __syncthreads();
@@ -127,7 +127,7 @@ struct Rs8Args {
 };
 
 __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t st[];  // [m][8][U]
+  extern __shared__ __attribute__((aligned(16))) uint32_t st[];  // [8][m][U] plane-major (conflict-free)
   const int U = a.U;
   int wg = blockIdx.x;
   const int slice = wg % a.slices;
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
       for (int j = 0; j < 8; j++) w[j] = 0;
     }
 #pragma unroll
-    for (int j = 0; j < 8; j++) st[(s * 8 + j) * U + u] = w[j];
+    for (int j = 0; j < 8; j++) st[j * (a.m << a.log2U) + s * U + u] = w[j];
   }
   __syncthreads();
   // IFFT (data at points m..m+k-1), D = 1 .. m/2
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
     const int s = e >> a.log2U, u = e & (U - 1);
     uint32_t w[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) w[j] = st[(s * 8 + j) * U + u];
+    for (int j = 0; j < 8; j++) w[j] = st[j * (a.m << a.log2U) + s * U + u];
     bitslice8(w);
     uint4* q = reinterpret_cast<uint4*>(dst + s * a.dst_sh + u * 32);
     q[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -505,8 +505,9 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
 // GF(2^16) encoder (klauspost leopardFF16 as selected for 2k > 256).
 // Element t of every 64-byte block = byte[t] | byte[t+32] << 8; a lane's unit is
 // one 64-byte block = 32 elements = 16 bit-planes (lo bytes -> planes 0..7, hi
-// bytes -> planes 8..15).  State for one codeword x U units lives in LDS
-// ([m][16][U] words); radix-2 layers as in the FF8 path.  Multiplication in the
+// bytes -> planes 8..15).  State for one codeword x U units lives in LDS as
+// [16][m][U] words (plane-major: the elements a wave touches in one plane are
+// contiguous, so LDS accesses are conflict-free); radix-2 layers as in FF8.  Multiplication in the
 // standard basis of GF(2)[x]/(x^16+x^5+x^3+x^2+1) (phi16 below), constant per
 // lane: masks from the constant's bits, or wave-uniform branches when all lanes
 // of the wave share the butterfly group (D*U >= 64).
@@ -570,12 +571,12 @@ __device__ __forceinline__ void gf16_muladd_lane(uint32_t (&X)[16], const uint32
 }
 
 template <bool INVERSE, bool UNIFORM>
-__device__ __forceinline__ void butterfly16(uint32_t* st, int U, int x, int y, int u, unsigned c) {
+__device__ __forceinline__ void butterfly16(uint32_t* st, int mU, int U, int x, int y, int u, unsigned c) {
   uint32_t X[16], Y[16];
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    X[j] = st[(x * 16 + j) * U + u];
-    Y[j] = st[(y * 16 + j) * U + u];
+    X[j] = st[j * mU + x * U + u];
+    Y[j] = st[j * mU + y * U + u];
   }
   if (INVERSE) {
 #pragma unroll
@@ -592,8 +593,8 @@ __device__ __forceinline__ void butterfly16(uint32_t* st, int U, int x, int y, i
   }
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    st[(x * 16 + j) * U + u] = X[j];
-    st[(y * 16 + j) * U + u] = Y[j];
+    st[j * mU + x * U + u] = X[j];
+    st[j * mU + y * U + u] = Y[j];
   }
 }
 
@@ -620,17 +621,17 @@ __device__ __forceinline__ void rs_layer16(uint32_t* st, const Rs16Args& a, int 
     const int idx = INVERSE ? (a.m - 1 + s0 + D) : (s0 + D - 1);
     if ((D << a.log2U) >= 64) {
       const int sidx = __builtin_amdgcn_readfirstlane(idx);
-      butterfly16<INVERSE, true>(st, U, x, y, u, a.cpoly[sidx]);
+      butterfly16<INVERSE, true>(st, a.m << a.log2U, U, x, y, u, a.cpoly[sidx]);
     } else {
-      butterfly16<INVERSE, false>(st, U, x, y, u, a.cpoly[idx]);
+      butterfly16<INVERSE, false>(st, a.m << a.log2U, U, x, y, u, a.cpoly[idx]);
     }
   }
   __syncthreads();
 }
 
 __global__ void __launch_bounds__(256) rs_encode16_kernel(Rs16Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t st[];  // [m][16][U]
-  const int U = a.U;
+  extern __shared__ __attribute__((aligned(16))) uint32_t st[];  // [16][m][U]
+  const int U = a.U, mU = a.m << a.log2U;
   int wg = blockIdx.x;
   const int slice = wg % a.slices;
   wg /= a.slices;
@@ -666,7 +667,7 @@ __global__ void __launch_bounds__(256) rs_encode16_kernel(Rs16Args a) {
       for (int j = 0; j < 16; j++) v[j] = 0;
     }
 #pragma unroll
-    for (int j = 0; j < 16; j++) st[(s * 16 + j) * U + u] = v[j];
+    for (int j = 0; j < 16; j++) st[j * mU + s * U + u] = v[j];
   }
   __syncthreads();
   for (int lD = 0; lD < a.log2m; lD++) rs_layer16<true>(st, a, 1 << lD, lD);
@@ -675,7 +676,7 @@ __global__ void __launch_bounds__(256) rs_encode16_kernel(Rs16Args a) {
     const int s = e >> a.log2U, u = e & (U - 1);
     uint32_t v[16];
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = st[(s * 16 + j) * U + u];
+    for (int j = 0; j < 16; j++) v[j] = st[j * mU + s * U + u];
     apply16(v, kPhiInv16);
     uint32_t lo[8], hi[8];
 #pragma unroll
