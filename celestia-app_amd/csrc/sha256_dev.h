@@ -143,4 +143,28 @@ __device__ __forceinline__ void sha256_compress_n(uint32_t (&s)[N][8], uint32_t 
   }
 }
 
+// One compression with scheduling fences every 8 rounds and after the block.
+// Straight-line code with several compressions (NMT inner nodes: 3 blocks)
+// otherwise lets the machine scheduler hoist later message-schedule words and
+// loads far ahead: 205 VGPRs (2 waves/SIMD) for the node kernel, 111 with fences.
+__device__ __forceinline__ void sha256_compress_fenced(uint32_t s[8], const uint32_t w[16]) {
+  uint32_t S[1][8], W[1][16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) S[0][i] = s[i];
+#pragma unroll
+  for (int i = 0; i < 16; i++) W[0][i] = w[i];
+  sha256_compress_n<1, 8>(S, W);
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = S[0][i];
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Opaque copy of a pointer: loads through it are neither merged with earlier
+// loads of the same address (CSE) nor kept live from them.
+template <typename T>
+__device__ __forceinline__ const T* launder(const T* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
 }  // namespace cda

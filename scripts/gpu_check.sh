@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU session: build check, parity tests, smoke, short bench.  Stops at the
-# first step that crashed/timed out (exit >= 124); a plain test failure (1) continues.
+# One GPU session: parity tests, smoke, short bench.  Stops at the first step
+# that crashed/timed out (exit >= 124); a plain test failure (1) continues.
 set -u
 mkdir -p gpurun_out
 run() {  # name timeout cmd...
@@ -12,6 +12,6 @@ run() {  # name timeout cmd...
   if [ $rc -ge 124 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-run tests 600 python -m pytest tests -m gpu -x -q
+run tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 400 python bench.py --steps 10 --warmup 2 --cpu-seconds 8
