@@ -11,3 +11,6 @@ DEFAULT_GOV_MAX_SQUARE_SIZE = 64          # initial_consts.go:10
 PARITY_SHARES_NAMESPACE = b"\xff" * 29                    # specs namespace.md:84
 TAIL_PADDING_NAMESPACE = b"\xff" * 28 + b"\xfe"           # specs namespace.md:83
 HASH_LENGTH = 32
+SUBTREE_ROOT_THRESHOLD = 64             # v1/app_consts.go:6 (SubtreeRootThreshold, versioned_consts.go:21-23)
+SHARE_VERSION_ZERO = 0
+SUPPORTED_SHARE_VERSIONS = (SHARE_VERSION_ZERO,)  # global_consts.go:94-95

@@ -533,3 +533,38 @@ void ora_gen_ods(int k, uint64_t seed, uint8_t* ods) {
   }
   qsort(ods, n, ORA_SHARE, share_cmp);
 }
+
+/* ------------------------------------------------------------------ */
+/* NMT building blocks for inclusion.c                                 */
+/* ------------------------------------------------------------------ */
+/* HashNode (hasher.go:271-310) for a namespace of ns_len bytes; ns_len = 29 is nmt_hash_node. */
+void ora_nmt_hash_node_ns(int ns_len, const uint8_t* l, const uint8_t* r, uint8_t* out) {
+  const int node = 2 * ns_len + 32;
+  uint8_t buf[1 + 2 * (2 * 64 + 32)], res[2 * 64 + 32];
+  int rmax = 1;
+  for (int i = 0; i < ns_len; i++) rmax &= r[i] == 0xFF;
+  buf[0] = 0x01;
+  memcpy(buf + 1, l, (size_t)node);
+  memcpy(buf + 1 + node, r, (size_t)node);
+  memcpy(res, l, (size_t)ns_len);
+  memcpy(res + ns_len, rmax ? l + ns_len : r + ns_len, (size_t)ns_len);
+  ora_sha256(buf, 1 + 2 * (size_t)node, res + 2 * ns_len);
+  memcpy(out, res, (size_t)node);
+}
+
+/* HashLeaf (hasher.go:186-209) of ns ‖ data: ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ data) */
+void ora_nmt_leaf_node(const uint8_t* ns, const uint8_t* data, size_t len, uint8_t* out) {
+  uint8_t* msg = (uint8_t*)malloc(1 + ORA_NS + len);
+  msg[0] = 0x00;
+  memcpy(msg + 1, ns, ORA_NS);
+  memcpy(msg + 1 + ORA_NS, data, len);
+  uint8_t node[ORA_NODE];
+  memcpy(node, ns, ORA_NS);
+  memcpy(node + ORA_NS, ns, ORA_NS);
+  ora_sha256(msg, 1 + ORA_NS + len, node + 2 * ORA_NS);
+  memcpy(out, node, ORA_NODE);
+  free(msg);
+}
+
+/* nmt computeRoot over n leaf nodes */
+void ora_nmt_root_of_nodes(const uint8_t* leaf_nodes, int n, uint8_t* out) { nmt_compute_root(leaf_nodes, 0, n, out); }

@@ -52,6 +52,8 @@ enum {
   ORA_E_BYZANTINE = -8,
   ORA_E_ARG = -9,
   ORA_E_PUSH_PAST = -11,
+  ORA_E_SHARE_VERSION = -13, /* appconsts.SupportedShareVersions / ErrUnsupportedShareVersion */
+  ORA_E_BLOB_SIZE = -14,     /* x/blob ErrZeroBlobSize */
 };
 
 /* ---- primitives ---- */
@@ -98,6 +100,31 @@ int ora_extend_commit(int count, size_t share_len, const uint8_t* shares, uint8_
  * Returns ORA_OK, ORA_E_UNREPAIRABLE or ORA_E_BYZANTINE (with axis/index). */
 int ora_repair(int k, size_t share_len, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, int* err_axis, int* err_index);
+
+/* ---- NMT building blocks (da.c) ---- */
+void ora_nmt_hash_node_ns(int ns_len, const uint8_t* l, const uint8_t* r, uint8_t* out);
+void ora_nmt_leaf_node(const uint8_t* ns, const uint8_t* data, size_t len, uint8_t* out);
+void ora_nmt_root_of_nodes(const uint8_t* leaf_nodes, int n, uint8_t* out);
+
+/* ---- blob share commitments, subtree roots and proofs (inclusion.c) ---- */
+int ora_sparse_shares_needed(uint32_t len);
+int ora_blob_to_shares(const uint8_t* ns, const uint8_t* data, uint32_t len, int share_version, uint8_t* out);
+int ora_blob_min_square_size(int share_count);
+int ora_subtree_width(int share_count, int threshold);
+int ora_mmr_sizes(int total, int max_tree, int* sizes);
+int ora_blob_commitment(const uint8_t* ns, const uint8_t* data, uint32_t len, int share_version, int threshold,
+                        uint8_t out[32]);
+int ora_subtree_root_coords(int max_depth, int min_depth, int start, int end, int* coords);
+void ora_axis_leaf_nodes(int k, const uint8_t* eds, int axis, int idx, uint8_t* out);
+void ora_nmt_tree_levels(const uint8_t* leaf_nodes, int n, uint8_t* out);
+int ora_get_commitment(int k, const uint8_t* eds, int start, int blob_share_len, int threshold, uint8_t out[32]);
+int ora_nmt_prove_range(const uint8_t* leaf_nodes, int n, int start, int end, uint8_t* out_nodes);
+int ora_nmt_verify_inclusion(int ns_len, const uint8_t* nid, const uint8_t* leaves, size_t leaf_len, int nleaves,
+                             int start, int end, const uint8_t* nodes, int nnodes, const uint8_t* root);
+int ora_merkle_proof(const uint8_t* items, size_t item_len, int n, int index, uint8_t leaf[32], uint8_t* aunts,
+                     uint8_t root[32]);
+int ora_merkle_verify(int64_t total, int64_t index, const uint8_t* proof_leaf_hash, const uint8_t* aunts, int na,
+                      const uint8_t* root, const uint8_t* item, size_t item_len);
 
 /* Deterministic generator used by tests and bench:
  * v0 namespaces (0x00 x19 ‖ 10 random bytes) ‖ 483 random bytes, sorted. */

@@ -282,7 +282,8 @@ def construct(txs):
     return ss, np.frombuffer(b"".join(square), np.uint8).reshape(ss * ss, SHARE), {
         "normal_txs": len(normal), "pfbs": len(pfbs), "blobs": len(blobs),
         "tx_shares": len(txs_sh), "pfb_shares": len(pfb_sh), "pfb_reserved": pfb_reserved,
-        "first_blob": non_reserved_start if blobs else None, "current_size": current}
+        "first_blob": non_reserved_start if blobs else None, "current_size": current,
+        "pfb_share_indexes": [p["idx"] for p in pfbs]}
 
 
 def main():

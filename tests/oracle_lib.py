@@ -20,6 +20,7 @@ NODE = 90
 OK, E_NOT_POW2, E_NOT_SQUARE, E_SHARD_SIZE, E_NS_SHORT, E_NS_ORDER, E_TOO_FEW, \
     E_UNREPAIRABLE, E_BYZANTINE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 E_PUSH_PAST = -11
+E_SHARE_VERSION, E_BLOB_SIZE = -13, -14
 
 
 def lib():
@@ -47,6 +48,7 @@ def lib():
         L.ora_extend_commit.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, ctypes.c_int]
         L.ora_repair.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, P]
         L.ora_gen_ods.argtypes = [ctypes.c_int, ctypes.c_uint64, P]
+        _bind_inclusion(L)
         _LIB = L
     return _LIB
 
@@ -168,3 +170,125 @@ def repair(eds: np.ndarray, present: np.ndarray, row_roots: np.ndarray, col_root
     rc = lib().ora_repair(w // 2, eds.shape[1], _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots)),
                           _p(np.ascontiguousarray(col_roots)), _p(ea), _p(ei))
     return rc, eds, pres, int(ea[0]), int(ei[0])
+
+
+# ---- blob share commitments, subtree roots and proofs (oracle/inclusion.c) ----------------
+def _bind_inclusion(L):
+    P, I, U32, SZ, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_int64
+    L.ora_sparse_shares_needed.argtypes = [U32]
+    L.ora_blob_to_shares.argtypes = [P, P, U32, I, P]
+    L.ora_subtree_width.argtypes = [I, I]
+    L.ora_blob_min_square_size.argtypes = [I]
+    L.ora_mmr_sizes.argtypes = [I, I, P]
+    L.ora_blob_commitment.argtypes = [P, P, U32, I, I, P]
+    L.ora_subtree_root_coords.argtypes = [I, I, I, I, P]
+    L.ora_axis_leaf_nodes.argtypes = [I, P, I, I, P]
+    L.ora_nmt_tree_levels.argtypes = [P, I, P]
+    L.ora_get_commitment.argtypes = [I, P, I, I, I, P]
+    L.ora_nmt_prove_range.argtypes = [P, I, I, I, P]
+    L.ora_nmt_verify_inclusion.argtypes = [I, P, P, SZ, I, I, I, P, I, P]
+    L.ora_merkle_proof.argtypes = [P, SZ, I, I, P, P, P]
+    L.ora_merkle_verify.argtypes = [I64, I64, P, P, I, P, P, SZ]
+    L.ora_nmt_hash_node_ns.argtypes = [I, P, P, P]
+    L.ora_nmt_leaf_node.argtypes = [P, P, SZ, P]
+    L.ora_nmt_root_of_nodes.argtypes = [P, I, P]
+
+
+def _buf(b):
+    b = bytes(b)
+    return np.frombuffer(b, np.uint8).copy() if b else np.zeros(1, np.uint8)
+
+
+def sparse_shares_needed(n):
+    return lib().ora_sparse_shares_needed(n)
+
+
+def blob_to_shares(ns, data, share_version=0):
+    """go-square SparseShareSplitter.Write: (n, 512) shares of one blob."""
+    n = lib().ora_sparse_shares_needed(len(data))
+    out = np.zeros((max(n, 1), SHARE), np.uint8)
+    lib().ora_blob_to_shares(_p(_buf(ns)), _p(_buf(data)), len(data), share_version, _p(out))
+    return out[:n]
+
+
+def subtree_width(share_count, threshold=64):
+    return lib().ora_subtree_width(share_count, threshold)
+
+
+def mmr_sizes(total, max_tree):
+    n = lib().ora_mmr_sizes(total, max_tree, None)
+    out = np.zeros(max(n, 1), np.int32)
+    lib().ora_mmr_sizes(total, max_tree, _p(out))
+    return [int(x) for x in out[:n]]
+
+
+def blob_commitment(ns, data, share_version=0, threshold=64):
+    """inclusion.CreateCommitment -> (rc, 32-byte commitment)."""
+    out = np.zeros(32, np.uint8)
+    rc = lib().ora_blob_commitment(_p(_buf(ns)), _p(_buf(data)), len(data), share_version, threshold, _p(out))
+    return rc, out.tobytes()
+
+
+def subtree_root_coords(max_depth, min_depth, start, end):
+    n = lib().ora_subtree_root_coords(max_depth, min_depth, start, end, None)
+    out = np.zeros(2 * n, np.int32)
+    lib().ora_subtree_root_coords(max_depth, min_depth, start, end, _p(out))
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+
+def axis_leaf_nodes(eds, axis, index):
+    """Erasured leaf nodes (2k, 90) of one EDS row (axis 0) or column (axis 1)."""
+    w = int(round(eds.shape[0] ** 0.5))
+    out = np.zeros((w, NODE), np.uint8)
+    lib().ora_axis_leaf_nodes(w // 2, _p(np.ascontiguousarray(eds)), axis, index, _p(out))
+    return out
+
+
+def tree_levels(leaf_nodes):
+    """All levels of the perfect NMT over n leaf nodes: (2n-1, 90), leaves first, root last."""
+    leaf_nodes = np.ascontiguousarray(leaf_nodes, np.uint8)
+    n = leaf_nodes.shape[0]
+    out = np.zeros((2 * n - 1, NODE), np.uint8)
+    lib().ora_nmt_tree_levels(_p(leaf_nodes), n, _p(out))
+    return out
+
+
+def get_commitment(eds, start, blob_share_len, threshold=64):
+    """pkg/inclusion GetCommitment over a full EDS -> (rc, 32 bytes)."""
+    w = int(round(eds.shape[0] ** 0.5))
+    out = np.zeros(32, np.uint8)
+    rc = lib().ora_get_commitment(w // 2, _p(np.ascontiguousarray(eds)), start, blob_share_len, threshold, _p(out))
+    return rc, out.tobytes()
+
+
+def nmt_prove_range(leaf_nodes, start, end):
+    """nmt ProveRange(start, end): list of 90-B proof nodes."""
+    leaf_nodes = np.ascontiguousarray(leaf_nodes, np.uint8)
+    out = np.zeros((128, NODE), np.uint8)
+    c = lib().ora_nmt_prove_range(_p(leaf_nodes), leaf_nodes.shape[0], start, end, _p(out))
+    if c < 0:
+        raise ValueError("invalid proof range")
+    return [out[i].tobytes() for i in range(c)]
+
+
+def nmt_verify_inclusion(nid, leaves, start, end, nodes, root):
+    """nmt Proof.VerifyInclusion (namespace size = len(nid))."""
+    leaf_len = len(leaves[0]) if leaves else 0
+    return bool(lib().ora_nmt_verify_inclusion(len(nid), _p(_buf(nid)), _p(_buf(b"".join(leaves))), leaf_len,
+                                               len(leaves), start, end, _p(_buf(b"".join(nodes))), len(nodes),
+                                               _p(_buf(root))))
+
+
+def merkle_proof(items, index):
+    """merkle.ProofsFromByteSlices(items)[index] -> (leaf_hash, aunts, root)."""
+    leaf, root = np.zeros(32, np.uint8), np.zeros(32, np.uint8)
+    aunts = np.zeros((100, 32), np.uint8)
+    na = lib().ora_merkle_proof(_p(_buf(b"".join(items))), len(items[0]), len(items), index, _p(leaf), _p(aunts),
+                                _p(root))
+    return leaf.tobytes(), [aunts[i].tobytes() for i in range(na)], root.tobytes()
+
+
+def merkle_verify(total, index, leaf_hash, aunts, root, item):
+    """merkle.Proof{Total, Index, LeafHash, Aunts}.Verify(root, item)."""
+    return bool(lib().ora_merkle_verify(total, index, _p(_buf(leaf_hash)), _p(_buf(b"".join(aunts))), len(aunts),
+                                        _p(_buf(root)), _p(_buf(item)), len(item)))

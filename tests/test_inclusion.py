@@ -1,0 +1,183 @@
+"""CPU tests: blob share commitments, subtree-root paths and proofs (oracle + host logic).
+
+The oracle (oracle/inclusion.c) is pinned here against the reference's own data:
+  * the share commitment of the blob in mainnet block 408
+    (x/blob/test/testdata/block_response.json -> tests/golden/make_blob_commitments.py),
+    through CreateCommitment and through GetCommitment over the block's EDS;
+  * the valid ShareProof / RowProof of pkg/proof/share_proof_test.go:74-93 and
+    row_proof_test.go:67-89 (tests/golden/make_share_proof_fixture.py).
+The path planning of the Python mirror (cda.inclusion) is checked against
+pkg/inclusion/paths_test.go.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from cda import inclusion as I
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+L, R = I.WALK_LEFT, I.WALK_RIGHT
+
+
+def mainnet_blobs():
+    z = np.load(os.path.join(GOLDEN, "mainnet_h408_blobs.npz"))
+    offs = z["offsets"]
+    return [dict(ns=z["namespaces"][i].tobytes(), data=z["data"][offs[i]:offs[i + 1]].tobytes(),
+                 version=int(z["share_versions"][i]), start=int(z["starts"][i]), n=int(z["nshares"][i]),
+                 commitment=z["commitments"][i].tobytes()) for i in range(len(offs) - 1)]
+
+
+def mainnet_ods():
+    return np.load(os.path.join(GOLDEN, "mainnet_h408.npz"))["ods"]
+
+
+# ---- paths_test.go -------------------------------------------------------------------------
+COORDS = [  # Test_calculateSubTreeRootCoordinates (paths_test.go:21-314): start, end, maxDepth, minDepth
+    (0, 4, 3, 1, [(1, 0)]), (4, 8, 3, 1, [(1, 1)]), (3, 5, 3, 3, [(3, 3), (3, 4)]), (3, 4, 3, 3, [(3, 3)]),
+    (3, 6, 3, 2, [(3, 3), (2, 2)]), (1, 7, 3, 2, [(3, 1), (2, 1), (2, 2), (3, 6)]),
+    (1, 7, 3, 3, [(3, 1), (3, 2), (3, 3), (3, 4), (3, 5), (3, 6)]), (0, 5, 3, 1, [(1, 0), (3, 4)]),
+    (0, 7, 3, 1, [(1, 0), (2, 2), (3, 6)]), (0, 8, 3, 0, [(0, 0)]), (0, 32, 7, 2, [(2, 0)]),
+    (0, 33, 7, 2, [(2, 0), (7, 32)]), (0, 31, 7, 3, [(3, 0), (4, 2), (5, 6), (6, 14), (7, 30)]),
+    (0, 64, 7, 1, [(1, 0)]), (0, 1, 2, 2, [(2, 0)]), (0, 19, 6, 3, [(3, 0), (3, 1), (5, 8), (6, 18)]),
+]
+
+
+@pytest.mark.parametrize("start,end,maxd,mind,want", COORDS)
+def test_subtree_root_coordinates(start, end, maxd, mind, want):
+    got = [(c.depth, c.position) for c in I.calculate_subtree_root_coordinates(maxd, mind, start, end)]
+    assert got == want
+    assert O.subtree_root_coords(maxd, mind, start, end) == want
+
+
+@pytest.mark.parametrize("depth,pos,want", [(2, 0, [L, L]), (0, 0, []), (3, 0, [L, L, L]), (3, 1, [L, L, R]),
+                                            (3, 2, [L, R, L]), (5, 16, [R, L, L, L, L])])
+def test_gen_subtree_root_path(depth, pos, want):  # paths_test.go:321-339
+    assert I.gen_subtree_root_path(depth, pos) == want
+
+
+PATHS = [  # Test_calculateCommitPaths (paths_test.go:352-450): squareSize, start, blobLen, {index: (row, path)}
+    (2, 2, 2, {0: (1, [L]), 1: (1, [R])}),
+    (4, 2, 2, {0: (0, [R, L]), 1: (0, [R, R])}),
+    (4, 3, 2, {0: (0, [R, R]), 1: (1, [L, L])}),
+    (128, 8252, 1, {0: (64, [L, R, R, R, R, L, L])}),
+    (128, 0, 8193, {31: (31, [])}),
+    (128, 0, 8192, {31: (31, [])}),
+    (128, 0, 64, {31: (0, [L, L, R, R, R, R, R])}),
+    (128, 0, 65, {31: (0, [L, R, R, R, R, R]), 32: (0, [R, L, L, L, L, L, L])}),
+]
+
+
+@pytest.mark.parametrize("square,start,n,want", PATHS)
+def test_calculate_commitment_paths(square, start, n, want):
+    paths = I.calculate_commitment_paths(square, start, n, 64)
+    for i, (row, instr) in want.items():
+        assert (paths[i].row, paths[i].instructions) == (row, instr)
+    keys = [(p.row, tuple(p.instructions)) for p in paths]
+    assert len(keys) == len(set(keys))  # every path is unique
+
+
+def test_share_arithmetic_mirror_matches_oracle():
+    # data_square_layout.md:58: 172 shares, SRT 64 -> width 4, 43 mountains of 4
+    assert I.sub_tree_width(172, 64) == O.subtree_width(172, 64) == 4
+    assert I.merkle_mountain_range_sizes(172, 4) == O.mmr_sizes(172, 4) == [4] * 43
+    for n in [1, 2, 3, 5, 17, 63, 64, 65, 127, 128, 129, 352, 1000, 4096, 8192, 8193, 16384]:
+        for t in [1, 8, 64]:
+            w = I.sub_tree_width(n, t)
+            assert w == O.subtree_width(n, t)
+            assert I.merkle_mountain_range_sizes(n, w) == O.mmr_sizes(n, w)
+            assert sum(I.merkle_mountain_range_sizes(n, w)) == n
+    for ln in [1, 477, 478, 479, 960, 961, 1_000_000]:
+        assert I.sparse_shares_needed(ln) == O.sparse_shares_needed(ln)
+    assert I.next_share_index(13, 4 * 64, 64) == 16
+
+
+# ---- commitments pinned on mainnet block 408 ----------------------------------------------
+def test_oracle_create_commitment_matches_mainnet_pfb():
+    blobs = mainnet_blobs()
+    assert blobs
+    for b in blobs:
+        rc, got = O.blob_commitment(b["ns"], b["data"], b["version"], 64)
+        assert rc == 0 and got == b["commitment"]
+
+
+def test_mainnet_blob_shares_sit_in_the_square():
+    ods = mainnet_ods()
+    for b in mainnet_blobs():
+        shares = O.blob_to_shares(b["ns"], b["data"], b["version"])
+        assert len(shares) == b["n"]
+        assert np.array_equal(shares, ods[b["start"]:b["start"] + b["n"]])
+
+
+def test_oracle_get_commitment_matches_mainnet_pfb():
+    eds = O.extend(mainnet_ods())
+    for b in mainnet_blobs():
+        rc, got = O.get_commitment(eds, b["start"], b["n"], 64)
+        assert rc == 0 and got == b["commitment"]
+
+
+def test_oracle_commitment_errors():
+    assert O.blob_commitment(bytes(29), b"", 0)[0] == O.E_BLOB_SIZE
+    assert O.blob_commitment(bytes(29), b"x", 1)[0] == O.E_SHARE_VERSION
+
+
+# ---- proof verifiers pinned on the reference's fixtures -----------------------------------
+def _fixture():
+    return json.load(open(os.path.join(GOLDEN, "share_proof_fixture.json")))
+
+
+def test_reference_row_proof_verifies():
+    fx = _fixture()
+    p, rr = fx["row_proof"], bytes.fromhex(fx["row_roots"][0])
+    aunts = [bytes.fromhex(a) for a in p["aunts"]]
+    args = (p["total"], p["index"], bytes.fromhex(p["leaf_hash"]), aunts)
+    assert O.merkle_verify(*args, bytes.fromhex(fx["root"]), rr)
+    assert not O.merkle_verify(*args, bytes(32), rr)  # incorrectRoot (row_proof_test.go:70)
+
+
+def test_reference_share_proof_verifies():
+    fx = _fixture()
+    rr = bytes.fromhex(fx["row_roots"][0])
+    nid = bytes([fx["namespace_version"]]) + bytes.fromhex(fx["namespace_id"])
+    data = [bytes.fromhex(d) for d in fx["data"]]
+    nodes = [bytes.fromhex(x) for x in fx["nmt"]["nodes"]]
+    s, e = fx["nmt"]["start"], fx["nmt"]["end"]
+    assert O.nmt_verify_inclusion(nid, data, s, e, nodes, rr)
+    bad = bytearray(data[0])
+    bad[100] ^= 1
+    assert not O.nmt_verify_inclusion(nid, [bytes(bad)], s, e, nodes, rr)
+    assert not O.nmt_verify_inclusion(nid, data, s, e, nodes[:-1], rr)
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8])
+def test_oracle_prove_range_round_trip(k):
+    """ProveRange over real erasured rows verifies against the row root for every range."""
+    eds = O.extend(O.gen_ods(k, 31 + k))
+    rc, rr, cr, *_ = O.roots(eds)
+    w = 2 * k
+    for row in {0, k - 1, w - 1}:
+        leaves = O.axis_leaf_nodes(eds, 0, row)
+        assert O.tree_levels(leaves)[-1].tobytes() == rr[row].tobytes()
+        cells = eds.reshape(w, w, 512)[row]
+        for s in range(w):
+            for e in range(s + 1, w + 1):
+                nodes = O.nmt_prove_range(leaves, s, e)
+                ns = leaves[s][:29].tobytes()
+                if any(leaves[i][:29].tobytes() != ns for i in range(s, e)):
+                    continue  # VerifyInclusion proves one namespace
+                assert O.nmt_verify_inclusion(ns, [cells[i].tobytes() for i in range(s, e)], s, e, nodes,
+                                              rr[row].tobytes())
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 13, 16])
+def test_oracle_merkle_proofs(n):
+    rng = np.random.default_rng(n)
+    items = [rng.integers(0, 256, 90, dtype=np.uint8).tobytes() for _ in range(n)]
+    want_root = O.merkle_root(items)
+    for i in range(n):
+        leaf, aunts, root = O.merkle_proof(items, i)
+        assert root == want_root
+        assert O.merkle_verify(n, i, leaf, aunts, root, items[i])
+        assert not O.merkle_verify(n, i, leaf, aunts, root, items[(i + 1) % n]) or n == 1
