@@ -31,6 +31,8 @@ E_ARG = -9
 E_DEVICE = -10
 E_PUSH_PAST = -11
 E_UNSUPPORTED = -12
+E_SHARE_VERSION = -13
+E_BLOB_SIZE = -14
 
 AXIS_ROW = 0
 AXIS_COL = 1
@@ -43,12 +45,18 @@ EXPORTS = [
     "cda_dah_hash", "cda_nmt_axis_root", "cda_repair",
     "cda_rs_encode_device", "cda_nmt_roots_device", "cda_nmt_fold_device", "cda_dah_device",
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
+    "cda_blob_commitments", "cda_merkle_roots", "cda_extend_commit_nodes", "cda_share_inclusion_proof",
 ]
 
 
 class ErrInfo(ctypes.Structure):
     _fields_ = [("code", ctypes.c_int32), ("axis", ctypes.c_int32), ("index", ctypes.c_int32),
                 ("leaf", ctypes.c_int32), ("block", ctypes.c_int32)]
+
+
+class ShareProofInfo(ctypes.Structure):
+    _fields_ = [("start_row", ctypes.c_uint32), ("end_row", ctypes.c_uint32), ("nrows", ctypes.c_uint32),
+                ("total", ctypes.c_uint32), ("naunts", ctypes.c_uint32), ("max_nodes", ctypes.c_uint32)]
 
 
 class CdaError(Exception):
@@ -97,6 +105,11 @@ def lib():
                 "cda_profile_enable": (I32, [P, I32]),
                 "cda_profile_read": (I32, [P, P, SZ, P, P, I32]),
                 "cda_profile_reset": (I32, [P]),
+                "cda_blob_commitments": (I32, [P, U32, P, P, P, P, U32, P, P]),
+                "cda_merkle_roots": (I32, [P, U32, P, P, U32, P]),
+                "cda_extend_commit_nodes": (I32, [P, U32, U32, P, P, P, P, P, P, P, P, P]),
+                "cda_share_inclusion_proof": (I32, [P, U32, U32, P, U32, U32, P, P, P, P, P, P, P, P, P,
+                                                      P]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)
@@ -264,6 +277,78 @@ class Context:
                               _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err))
         _check(rc, err, self)
         return eds, pres
+
+    # ---- blob share commitments, node export, proofs ----
+    def blob_commitments(self, namespaces, datas, share_versions=None, subtree_root_threshold=64):
+        """inclusion.CreateCommitments over many blobs in one call -> list of 32-byte commitments."""
+        nb = len(datas)
+        if nb == 0:
+            return []
+        ns = np.frombuffer(b"".join(bytes(n) for n in namespaces), np.uint8).copy()
+        if ns.size != nb * NAMESPACE_SIZE:
+            raise CdaError(E_ARG, "namespaces must be 29 bytes each")
+        flat = b"".join(bytes(d) for d in datas)
+        data = np.frombuffer(flat, np.uint8).copy() if flat else np.zeros(1, np.uint8)
+        offs = np.zeros(nb + 1, np.uint64)
+        offs[1:] = np.cumsum([len(d) for d in datas])
+        sv = None if share_versions is None else np.ascontiguousarray(share_versions, np.uint8)
+        out = np.empty((nb, 32), np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_blob_commitments(self._h, nb, _p(ns), _p(data), _p(offs), _p(sv), subtree_root_threshold,
+                                        _p(out), ctypes.byref(err))
+        _check(rc, err, self)
+        return [bytes(o) for o in out]
+
+    def merkle_roots(self, sets):
+        """merkle.HashFromByteSlices of each list of 90-byte NMT nodes."""
+        offs = np.zeros(len(sets) + 1, np.uint32)
+        offs[1:] = np.cumsum([len(x) for x in sets])
+        flat = b"".join(bytes(x) for st in sets for x in st)
+        items = np.frombuffer(flat, np.uint8).copy() if flat else None
+        out = np.empty((len(sets), 32), np.uint8)
+        _check(lib().cda_merkle_roots(self._h, len(sets), _p(offs), _p(items), NODE_SIZE, _p(out)), ctx=self)
+        return [bytes(o) for o in out]
+
+    def extend_commit_nodes(self, shares, want_eds=False, rows=True, cols=True, dah_tree=True):
+        """extend_commit plus every node of the row / column NMTs and of the DAH tree."""
+        shares = np.ascontiguousarray(shares, np.uint8)
+        count, L = shares.shape
+        w = 2 * max(1, int(round(count ** 0.5)))
+        eds = np.empty((w * w, L), np.uint8) if want_eds else None
+        rr, cr = np.empty((w, NODE_SIZE), np.uint8), np.empty((w, NODE_SIZE), np.uint8)
+        dah = np.empty(32, np.uint8)
+        rn = np.empty((w, 2 * w - 1, NODE_SIZE), np.uint8) if rows else None
+        cn = np.empty((w, 2 * w - 1, NODE_SIZE), np.uint8) if cols else None
+        dn = np.empty((4 * w - 1, 32), np.uint8) if dah_tree else None
+        err = ErrInfo()
+        rc = lib().cda_extend_commit_nodes(self._h, count, L, _p(shares), _p(eds), _p(rr), _p(cr), _p(dah), _p(rn),
+                                           _p(cn), _p(dn), ctypes.byref(err))
+        _check(rc, err, self)
+        return {"eds": eds, "row_roots": rr, "col_roots": cr, "dah": dah.tobytes(), "row_nodes": rn,
+                "col_nodes": cn, "dah_nodes": dn}
+
+    def share_inclusion_proof(self, shares, start, end):
+        """pkg/proof NewShareInclusionProof for ODS shares [start, end) (raw proof parts)."""
+        shares = np.ascontiguousarray(shares, np.uint8)
+        count, L = shares.shape
+        k = max(1, int(round(count ** 0.5)))
+        lg = (2 * k).bit_length() - 1
+        info = ShareProofInfo()
+        rr, lh = np.empty((k, NODE_SIZE), np.uint8), np.empty((k, 32), np.uint8)
+        au = np.empty((k, lg + 1, 32), np.uint8)
+        ns, ne, nc = np.empty(k, np.int32), np.empty(k, np.int32), np.empty(k, np.int32)
+        nodes = np.empty((k, 2 * lg, NODE_SIZE), np.uint8)
+        root = np.empty(32, np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_share_inclusion_proof(self._h, count, L, _p(shares), start, end, ctypes.byref(info), _p(rr),
+                                             _p(lh), _p(au), _p(ns), _p(ne), _p(nc), _p(nodes), _p(root),
+                                             ctypes.byref(err))
+        _check(rc, err, self)
+        rows = [{"row_root": rr[i].tobytes(), "leaf_hash": lh[i].tobytes(),
+                 "aunts": [au[i, j].tobytes() for j in range(info.naunts)], "start": int(ns[i]), "end": int(ne[i]),
+                 "nodes": [nodes[i, j].tobytes() for j in range(nc[i])]} for i in range(info.nrows)]
+        return {"start_row": info.start_row, "end_row": info.end_row, "total": info.total, "rows": rows,
+                "data_root": root.tobytes()}
 
     # ---- profiling ----
     def profile_enable(self, on=True):

@@ -89,6 +89,61 @@ class DataAvailabilityHeader:
             raise DAError("wrong hash: expected size to be 32 bytes")
 
 
+    def to_proto(self):
+        """ToProto (:110-119) in wire form: celestia.core.v1.da.DataAvailabilityHeader
+        {repeated bytes row_roots = 1; repeated bytes column_roots = 2}
+        (proto/celestia/core/v1/da/data_availability_header.proto:16-21)."""
+        out = bytearray()
+        for r in self.row_roots:
+            out += b"\x0a" + _varint(len(r)) + r
+        for c in self.column_roots:
+            out += b"\x12" + _varint(len(c)) + c
+        return bytes(out)
+
+
+def _varint(v):
+    out = bytearray()
+    while True:
+        b, v = v & 0x7F, v >> 7
+        out.append(b | 0x80 if v else b)
+        if not v:
+            return bytes(out)
+
+
+def _read_varint(buf, i):
+    shift = v = 0
+    while True:
+        if i >= len(buf):
+            raise DAError("truncated varint")
+        b = buf[i]
+        i += 1
+        v |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            return v, i
+
+
+def data_availability_header_from_proto(buf, ctx=None):
+    """DataAvailabilityHeaderFromProto (:121-131): decode the wire message, then ValidateBasic."""
+    buf = bytes(buf)
+    rows, cols, i = [], [], 0
+    while i < len(buf):
+        key, i = _read_varint(buf, i)
+        if key & 7 != 2:
+            raise DAError(f"unexpected wire type {key & 7}")
+        n, i = _read_varint(buf, i)
+        if i + n > len(buf):
+            raise DAError("truncated DataAvailabilityHeader")
+        if key >> 3 == 1:
+            rows.append(buf[i:i + n])
+        elif key >> 3 == 2:
+            cols.append(buf[i:i + n])
+        i += n
+    dah = DataAvailabilityHeader(rows, cols, ctx=ctx)
+    dah.validate_basic()
+    return dah
+
+
 def new_data_availability_header(eds: ExtendedDataSquare):
     """NewDataAvailabilityHeader (:44-63)."""
     dah = DataAvailabilityHeader(eds.row_roots(), eds.col_roots(), ctx=eds.codec.ctx)

@@ -70,6 +70,29 @@ int launch_nmt_fold(void* d_nodes, void* d_scratch, void* d_roots, int ntrees, i
 int launch_parity_compare(const uint8_t* d_eds, int k, const int* d_axes, int naxes, const uint8_t* d_par,
                           unsigned* d_flags, hipStream_t s);
 
+// Blob of a share-commitment batch (go-square inclusion.CreateCommitment), built by the host.
+struct BlobDesc {
+  unsigned long long data_off;  // first data byte in the call's data buffer
+  uint32_t len;                 // data bytes (> 0)
+  uint32_t share_off;           // first share of the blob in the call's share buffer
+  uint32_t nshares;             // shares.SparseSharesNeeded(len)
+  uint32_t width;               // SubTreeWidth(nshares, threshold), a power of two
+  uint8_t ns[32];               // namespace (29 B); share version at [29]
+};
+// sparse shares of every blob, contiguous (total shares x 512 B)
+int launch_blob_shares(const BlobDesc* d_desc, int nblobs, const uint8_t* d_data, uint32_t total, uint8_t* d_shares,
+                       hipStream_t s);
+// 96-B leaf records of shares whose namespace is their own (ns ‖ share leaves)
+int launch_blob_leaves(const uint8_t* d_shares, uint32_t total, void* d_recs, hipStream_t s);
+// one level of every mountain of every blob, folded in place
+int launch_blob_mountain_level(const BlobDesc* d_desc, int nblobs, void* d_recs, uint32_t total, int level,
+                               hipStream_t s);
+// RFC-6962 root (merkle.HashFromByteSlices) of each set of 90-B node records: set s =
+// records idx[off[s] .. off[s+1]) (idx == null: records off[s] ..).  out: nsets x 32 B.
+// nodes_out (nsets == 1 only): every level's 32-B digests, leaves first.  -2: set too large.
+int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t* d_off, int nsets, int max_set,
+                       void* d_out, void* d_nodes_out, hipStream_t s);
+
 // profiling hook implemented by the engine
 struct ProfScope {
   void* ctx;

@@ -1,0 +1,67 @@
+// ctx.h — libcda host context and helpers shared by engine.cpp (block path,
+// codec, repair) and inclusion.cpp (blob commitments, node export, proofs).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cda_internal.h"
+
+struct cda_ctx {
+  int device = 0;
+  std::recursive_mutex mu;
+  hipStream_t stream = nullptr;
+  // sub-batch streams: independent blocks of one call are split across these so
+  // that one sub-batch's memory-bound RS phase and latency-bound tree tail overlap
+  // another's hashing (no dependency between blocks).
+  static constexpr int kMaxSub = 8;
+  int nsub = 1;
+  hipStream_t sub[kMaxSub] = {};
+  hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
+  std::string last_err;
+  // workspace
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Buf ods, eds, leaf, scratch, roots, dah, status, host_status;
+  // profiling
+  bool prof = false;
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  std::map<std::string, std::pair<double, long long>> prof_acc;
+};
+
+namespace cda {
+
+// Largest ODS width on the device block path: FF16 codewords up to m = 2048 in
+// LDS, DAH tree of 4k roots in one workgroup's LDS (k <= 512).
+constexpr uint32_t kMaxDeviceK = 512;
+
+bool dev_ok(cda_ctx* c, hipError_t e, const char* what);
+int ensure(cda_ctx* c, cda_ctx::Buf& b, size_t bytes);
+void flush_profile(cda_ctx* c);
+int ilog2i(uint32_t v);
+bool is_pow2(uint64_t v);
+void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block);
+// 96-B records -> packed 90-B nodes
+void pack_roots(const uint8_t* recs, uint32_t n, uint8_t* out);
+// device status word -> CDA_OK / CDA_E_NS_ORDER (+ err detail)
+int map_status(uint64_t st, int block, cda_err_info* err);
+// RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
+int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
+
+struct Lock {
+  cda_ctx* c;
+  std::lock_guard<std::recursive_mutex> g;
+  explicit Lock(cda_ctx* x) : c(x), g(x->mu) { (void)hipSetDevice(x->device); }
+};
+
+}  // namespace cda

@@ -23,36 +23,8 @@
 #include <string>
 #include <vector>
 
-#include "cda_internal.h"
+#include "ctx.h"
 
-struct cda_ctx {
-  int device = 0;
-  std::recursive_mutex mu;
-  hipStream_t stream = nullptr;
-  // sub-batch streams: independent blocks of one call are split across these so
-  // that one sub-batch's memory-bound RS phase and latency-bound tree tail overlap
-  // another's hashing (no dependency between blocks).
-  static constexpr int kMaxSub = 8;
-  int nsub = 1;
-  hipStream_t sub[kMaxSub] = {};
-  hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
-  std::string last_err;
-  // workspace
-  struct Buf {
-    void* p = nullptr;
-    size_t cap = 0;
-  };
-  Buf ods, eds, leaf, scratch, roots, dah, status, host_status;
-  // profiling
-  bool prof = false;
-  struct Pending {
-    std::string name;
-    hipEvent_t a, b;
-  };
-  std::vector<Pending> pending;
-  std::vector<hipEvent_t> event_pool;
-  std::map<std::string, std::pair<double, long long>> prof_acc;
-};
 
 namespace cda {
 
@@ -85,7 +57,7 @@ ProfScope::~ProfScope() {
 
 using namespace cda;
 
-namespace {
+namespace cda {
 
 bool dev_ok(cda_ctx* c, hipError_t e, const char* what) {
   if (e == hipSuccess) return true;
@@ -126,9 +98,6 @@ int ilog2i(uint32_t v) {
 }
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
-// Largest ODS width on the device block path: FF16 codewords up to m = 2048 in
-// LDS, DAH tree of 4k roots in one workgroup's LDS (k <= 512).
-constexpr uint32_t kMaxDeviceK = 512;
 
 void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block) {
   if (!e) return;
@@ -280,13 +249,8 @@ int map_status(uint64_t st, int block, cda_err_info* err) {
   return CDA_E_NS_ORDER;
 }
 
-struct Lock {
-  cda_ctx* c;
-  std::lock_guard<std::recursive_mutex> g;
-  explicit Lock(cda_ctx* x) : c(x), g(x->mu) { (void)hipSetDevice(x->device); }
-};
 
-}  // namespace
+}  // namespace cda
 
 extern "C" {
 
@@ -356,6 +320,8 @@ const char* cda_strerror(int code) {
     case CDA_E_DEVICE: return "device error";
     case CDA_E_PUSH_PAST: return "pushed past predetermined square size";
     case CDA_E_UNSUPPORTED: return "unsupported configuration";
+    case CDA_E_SHARE_VERSION: return "unsupported share version";
+    case CDA_E_BLOB_SIZE: return "cannot use zero blob size";
     default: return "unknown error";
   }
 }

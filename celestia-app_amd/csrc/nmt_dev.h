@@ -157,4 +157,90 @@ __device__ __forceinline__ void leaf_cell(const uint8_t* __restrict__ eds, uint4
   leaf_record(sh, A, q0, nodes + (size_t)gid * 6);
 }
 
+// ---------------------------------------------------------------------------
+// Inner NMT node (also the in-place mountain fold of inclusion_kernels.hip).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ld4(const uint4* p, uint32_t* w) {  // 4 x 16 B -> 16 words
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint4 v = p[i];
+    w[4 * i + 0] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+
+// Inner node from the two child records at pl / pr, written to po.  The
+// children are read block by block (through laundered pointers, so the reads
+// are not merged and kept live) and each compression is fenced: 111 VGPRs
+// instead of 205 for the version that held both children in registers.
+__device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po) {
+  uint32_t st[8], m[16];
+  sha256_init(st);
+  // message = 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits); 48 words
+  {  // block 0: words 0..15 <- L words 0..15
+    uint32_t L[16];
+    ld4(launder(pl), L);
+    m[0] = be_window(0x01000000u, L[0], 3);
+#pragma unroll
+    for (int i = 1; i < 16; i++) m[i] = be_window(L[i - 1], L[i], 3);
+  }
+  sha256_compress_fenced(st, m);
+  {  // block 1: words 16..31 <- L words 15..22, R words 0..8
+    uint32_t L[16], R[16];  // L words 12..27, R words 0..15
+    ld4(launder(pl) + 3, L);  // words 12..27: only 12..23 are read
+    ld4(launder(pr), R);      // words 0..15: only 0..11 are read
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int wi = 16 + i;
+      if (wi <= 21) m[i] = be_window(L[wi - 13], L[wi - 12], 3);
+      else if (wi == 22) m[i] = be_window(L[9], L[10], 3) | (R[0] & 0xFFu);
+      else m[i] = be_window(R[wi - 23], R[wi - 22], 1);
+    }
+  }
+  sha256_compress_fenced(st, m);
+  {  // block 2: words 32..47 <- R words 8..23
+    uint32_t R[16];
+    ld4(launder(pr) + 2, R);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int wi = 32 + i;
+      if (wi <= 44) m[i] = be_window(R[wi - 31], R[wi - 30], 1);
+      else if (wi == 45) m[i] = be_window(R[14], R[15], 1) | 0x00800000u;
+      else if (wi == 46) m[i] = 0;
+      else m[i] = 181u * 8u;
+    }
+  }
+  sha256_compress_fenced(st, m);
+
+  // namespace range: min = L.min; max = R.min == parity ns ? L.max : R.max
+  uint32_t L[16], R[16];
+  ld4(launder(pl), L);
+  ld4(launder(pr), R);
+  bool rmin_max = true;
+#pragma unroll
+  for (int i = 0; i < 7; i++) rmin_max &= (R[i] == 0xFFFFFFFFu);
+  rmin_max &= ((R[7] & 0xFFu) == 0xFFu);
+  uint32_t S[16];
+#pragma unroll
+  for (int i = 7; i < 15; i++) S[i] = rmin_max ? L[i] : R[i];
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = bswap(st[i]);
+  uint32_t o[24];
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = L[i];
+  o[7] = (L[7] & 0xFFu) | (S[7] & 0xFFFFFF00u);
+#pragma unroll
+  for (int i = 8; i < 14; i++) o[i] = S[i];
+  o[14] = (S[14] & 0xFFFFu) | (d[0] << 16);
+#pragma unroll
+  for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
+  o[22] = d[7] >> 16;
+  o[23] = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
+
 }  // namespace cda

@@ -41,6 +41,8 @@ enum {
   CDA_E_DEVICE = -10,      /* HIP runtime / device failure */
   CDA_E_PUSH_PAST = -11,   /* wrapper Push "pushed past predetermined square size" (nmt_wrapper.go:94-96) */
   CDA_E_UNSUPPORTED = -12, /* configuration not implemented on the device path */
+  CDA_E_SHARE_VERSION = -13, /* x/blob ErrUnsupportedShareVersion (appconsts.SupportedShareVersions = {0}) */
+  CDA_E_BLOB_SIZE = -14,     /* x/blob ErrZeroBlobSize: empty blob data (x/blob/types/payforblob.go:230-232) */
 };
 
 enum { CDA_AXIS_ROW = 0, CDA_AXIS_COL = 1 }; /* rsmt2d.Row / rsmt2d.Col */
@@ -163,6 +165,55 @@ int cda_nmt_axis_root(cda_ctx* ctx, uint64_t square_size, uint64_t axis_index, u
  * CDA_E_BYZANTINE (err->axis/index). */
 int cda_repair(cda_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, cda_err_info* err);
+
+/* ---- blob share commitments (x/blob, go-square inclusion) -------------- */
+/* inclusion.CreateCommitments(blobs, merkle.HashFromByteSlices, threshold)
+ * (x/blob/types/payforblob.go:53; CreateCommitment per blob in ValidateBlobTx,
+ * blob_tx.go:97-105).  Blob b = namespace namespaces[29b, 29b+29) and data
+ * data[offsets[b], offsets[b+1]); share_versions may be NULL (all 0).
+ * commitments: nblobs x 32 B.  Errors name the blob in err->index, checked in
+ * ValidateBlobs' order (payforblob.go:230-236): CDA_E_BLOB_SIZE, CDA_E_SHARE_VERSION. */
+int cda_blob_commitments(cda_ctx* ctx, uint32_t nblobs, const uint8_t* namespaces, const uint8_t* data,
+                         const uint64_t* offsets, const uint8_t* share_versions, uint32_t subtree_root_threshold,
+                         uint8_t* commitments, cda_err_info* err);
+
+/* merkle.HashFromByteSlices over sets of 90-B NMT nodes (the subtree-root fold of
+ * pkg/inclusion/get_commit.go:29): set s = items[off[s]-off[0], off[s+1]-off[0]);
+ * roots: nsets x 32 B; an empty set hashes to SHA256("").  item_len must be 90. */
+int cda_merkle_roots(cda_ctx* ctx, uint32_t nsets, const uint32_t* set_offsets, const uint8_t* items,
+                     uint32_t item_len, uint8_t* roots);
+
+/* ---- NMT node export and share inclusion proofs (pkg/inclusion, pkg/proof) ---- */
+/* cda_extend_commit plus every node of the trees the block path builds: what the
+ * inner-node cache of pkg/inclusion/nmt_caching.go:76-124 records through nmt's
+ * NodeVisitor, and what pkg/proof/proof.go:82-153 recomputes for proofs.
+ * row_nodes / col_nodes (optional): 2k trees x (4k-1) nodes x 90 B; per tree the
+ * 2k leaves first, then each level, the root last.  dah_nodes (optional):
+ * (8k-1) x 32 B, the RFC-6962 tree over rowRoots ‖ colRoots, leaf hashes first,
+ * the data root last. */
+int cda_extend_commit_nodes(cda_ctx* ctx, uint32_t count, uint32_t share_len, const uint8_t* shares,
+                            uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                            uint8_t* row_nodes, uint8_t* col_nodes, uint8_t* dah_nodes, cda_err_info* err);
+
+typedef struct {
+  uint32_t start_row, end_row; /* RowProof.StartRow / EndRow */
+  uint32_t nrows;              /* end_row - start_row + 1 */
+  uint32_t total;              /* Proof.Total = 4k (rowRoots ‖ colRoots) */
+  uint32_t naunts;             /* aunts per row proof = log2(4k) */
+  uint32_t max_nodes;          /* node slots per row in nmt_nodes = 2 log2(2k) */
+} cda_share_proof_info;
+
+/* pkg/proof NewShareInclusionProof (proof.go:55-167) for the ODS shares
+ * [start, end) of the k x k square `shares` (count = k*k).  Per proven row i
+ * (capacity k rows): row_roots 90 B; the row root's RFC-6962 proof in the data
+ * root (merkle.ProofsFromByteSlices, :82-93): leaf_hashes 32 B, aunts naunts x 32 B
+ * bottom-up; the NMT range proof (ProveRange, :129-152): nmt_start / nmt_end /
+ * nmt_count and nmt_nodes (max_nodes x 90-B slots, left to right).  data_root
+ * (optional): the DAH hash.  ShareProof.Data is the caller's input range. */
+int cda_share_inclusion_proof(cda_ctx* ctx, uint32_t count, uint32_t share_len, const uint8_t* shares, uint32_t start,
+                              uint32_t end, cda_share_proof_info* info, uint8_t* row_roots, uint8_t* leaf_hashes,
+                              uint8_t* aunts, int32_t* nmt_start, int32_t* nmt_end, int32_t* nmt_count,
+                              uint8_t* nmt_nodes, uint8_t* data_root, cda_err_info* err);
 
 /* ---- instrumentation ----------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed by HIP events on its own
