@@ -151,6 +151,46 @@ def repair_measure(ctx, k=128, survive=0.5, reps=3):
             "note": "cda_repair incl. 32 MiB H2D + D2H of the EDS; PCIe-inclusive"}
 
 
+# bench kernel name -> rocprofv3 kernel name in profiles/*_counters.json
+PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "nmt_level1": "nmt_level_kernel<true>", "dah": "dah_kernel"}
+
+
+def pmc_traffic(kernel, B):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary (profiles/r01_*_counters.json,
+    hbm_bytes_corrected = 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), measured on
+    this bench at B = 128 and scaled to the batch; None when no profile covers the kernel."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_*_counters.json")))
+    if not files or kernel not in PMC_NAMES:
+        return None
+    try:
+        c = json.load(open(files[-1])).get(PMC_NAMES[kernel])
+    except (OSError, ValueError):
+        return None
+    if not c or "hbm_bytes_corrected" not in c:
+        return None
+    return {"bytes": int(c["hbm_bytes_corrected"] * B / 128),
+            "source": f"{os.path.relpath(files[-1], ROOT)} ({PMC_NAMES[kernel]}, B=128 profile scaled to B={B})"}
+
+
+def commitments_measure(ctx, nblobs=256, size=64 * 1024, reps=3):
+    """x/blob share commitments (inclusion.CreateCommitments) for a batch of random blobs through
+    cda_blob_commitments; host buffers in and out (PCIe-inclusive)."""
+    rng = np.random.default_rng(11)
+    datas = [rng.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(nblobs)]
+    ns = [bytes(19) + rng.integers(0, 256, 10, dtype=np.uint8).tobytes() for _ in range(nblobs)]
+    ctx.blob_commitments(ns, datas)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.blob_commitments(ns, datas)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    return {"blobs": nblobs, "blob_bytes": size, "ms": round(best * 1e3, 2),
+            "blobs_per_s": round(nblobs / best, 1), "mb_per_s": round(nblobs * size / best / 1e6, 1),
+            "note": "cda_blob_commitments incl. H2D of the blob data; threshold 64"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -281,8 +321,13 @@ def main():
         "sha256_compressions_per_s": comp_per_s,
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
+    traffic = pmc_traffic(dom, B)
+    if traffic:
+        result["roofline"]["traffic"] = traffic["bytes"]
+        result["roofline"]["traffic_source"] = traffic["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["repair_c4"] = repair_measure(ctx)
+        result["blob_commitments"] = commitments_measure(ctx)
         result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
