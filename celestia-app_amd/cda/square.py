@@ -1,0 +1,246 @@
+"""go-square square construction mirror: transactions -> original data square (ODS).
+
+The step before the DA path: app/prepare_proposal.go:54 and
+app/process_proposal.go:121 call go-square v1.0.1 square.Construct / Build and
+shares.ToBytes (go.mod:9, not vendored), then da.ExtendShares. The rules are
+restated from the reference's specs and call sites:
+
+  * txs split into normal txs and BlobTxs (blob.UnmarshalBlobTx: BlobTx{tx=1,
+    blobs=2, type_id=3 "BLOB"}); blobs sorted stably by namespace, PFB priority
+    order kept within a namespace (test/util/malicious/out_of_order_builder.go:24-150
+    is the builder and its Export, here without the malicious swap);
+  * compact shares for the TRANSACTION and PAY_FOR_BLOB namespaces: varint-delimited
+    units, sequence length and reserved bytes (specs/src/specs/shares.md:61-80);
+    PFBs are wrapped in IndexWrapper{tx=1, share_indexes=2, type_id=3 "INDX"};
+  * sparse blob shares, namespace / reserved / tail padding (shares.md:31-122);
+  * every blob starts at a multiple of its SubTreeWidth
+    (specs/src/specs/data_square_layout.md:47-60);
+  * the PFB share reservation assumes worst-case share indexes of
+    SquareSizeUpperBound^2 (pkg/appconsts/v1/app_consts.go:5).
+
+Pinned on real data: mainnet block 408's txs (the reference's fixture
+x/blob/test/testdata/block_response.json) construct the square whose DAH is the
+block header's data_hash (tests/test_square.py). Host logic only: the bytes are
+layout, not arithmetic; the extension and hashing run in libcda.
+"""
+import math
+
+from . import appconsts
+from .inclusion import next_share_index, sparse_shares_needed, sub_tree_width
+
+SHARE = appconsts.SHARE_SIZE
+NS = appconsts.NAMESPACE_SIZE
+TX_NAMESPACE = bytes(28) + b"\x01"
+PAY_FOR_BLOB_NAMESPACE = bytes(28) + b"\x04"
+PRIMARY_RESERVED_PADDING_NAMESPACE = bytes(28) + b"\xff"
+TAIL_PADDING_NAMESPACE = appconsts.TAIL_PADDING_NAMESPACE
+FIRST_COMPACT_SHARE_CONTENT_SIZE = SHARE - NS - 1 - 4 - 4  # 474
+CONTINUATION_COMPACT_SHARE_CONTENT_SIZE = SHARE - NS - 1 - 4  # 478
+
+
+class SquareError(Exception):
+    pass
+
+
+# ---- protobuf wire format --------------------------------------------------------------------
+def varint(v):
+    out = bytearray()
+    while True:
+        b, v = v & 0x7F, v >> 7
+        out.append(b | 0x80 if v else b)
+        if not v:
+            return bytes(out)
+
+
+def read_varint(buf, i):
+    shift = v = 0
+    while True:
+        b = buf[i]
+        i += 1
+        v |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            return v, i
+
+
+def parse_fields(buf):
+    """-> list of (field, wire type, value), or None if `buf` is not a well-formed message."""
+    out, i = [], 0
+    try:
+        while i < len(buf):
+            key, i = read_varint(buf, i)
+            f, wt = key >> 3, key & 7
+            if wt == 0:
+                v, i = read_varint(buf, i)
+            elif wt == 2:
+                n, i = read_varint(buf, i)
+                if i + n > len(buf):
+                    return None
+                v, i = bytes(buf[i:i + n]), i + n
+            elif wt == 1:
+                v, i = bytes(buf[i:i + 8]), i + 8
+            elif wt == 5:
+                v, i = bytes(buf[i:i + 4]), i + 4
+            else:
+                return None
+            if f == 0:
+                return None
+            out.append((f, wt, v))
+    except IndexError:
+        return None
+    return out
+
+
+def unmarshal_blob_tx(raw):
+    """blob.UnmarshalBlobTx -> (tx, [{"ns", "data", "share_version"}]) or None for a normal tx."""
+    fields = parse_fields(raw)
+    if fields is None:
+        return None
+    tx, blobs, type_id = b"", [], b""
+    for f, wt, v in fields:
+        if f == 1 and wt == 2:
+            tx = v
+        elif f == 2 and wt == 2:
+            blobs.append(v)
+        elif f == 3 and wt == 2:
+            type_id = v
+    if type_id != b"BLOB" or not blobs:
+        return None
+    parsed = []
+    for b in blobs:
+        ns_id, data, share_version, ns_version = b"", b"", 0, 0
+        for f, wt, v in parse_fields(b) or []:
+            if f == 1:
+                ns_id = v
+            elif f == 2:
+                data = v
+            elif f == 3:
+                share_version = v
+            elif f == 4:
+                ns_version = v
+        parsed.append({"ns": bytes([ns_version]) + ns_id, "data": data, "share_version": share_version})
+    return tx, parsed
+
+
+def marshal_index_wrapper(tx, share_indexes):
+    """blob.MarshalIndexWrapper: IndexWrapper{tx=1, share_indexes=2 (packed), type_id=3 "INDX"}."""
+    out = b"\x0a" + varint(len(tx)) + tx
+    if share_indexes:
+        packed = b"".join(varint(x) for x in share_indexes)
+        out += b"\x12" + varint(len(packed)) + packed
+    return out + b"\x1a" + varint(4) + b"INDX"
+
+
+# ---- shares ------------------------------------------------------------------------------------
+def compact_shares_needed(sequence_len):
+    if sequence_len == 0:
+        return 0
+    if sequence_len <= FIRST_COMPACT_SHARE_CONTENT_SIZE:
+        return 1
+    return 1 + math.ceil((sequence_len - FIRST_COMPACT_SHARE_CONTENT_SIZE) / CONTINUATION_COMPACT_SHARE_CONTENT_SIZE)
+
+
+def compact_shares(ns, units):
+    """CompactShareSplitter: varint-delimited units, sequence length, reserved bytes (shares.md:61-80)."""
+    seq = b"".join(varint(len(u)) + u for u in units)
+    starts, off = [], 0
+    for u in units:
+        starts.append(off)
+        off += len(varint(len(u))) + len(u)
+    out, pos = [], 0
+    for s in range(compact_shares_needed(len(seq))):
+        first = s == 0
+        header = ns + bytes([1 if first else 0]) + (len(seq).to_bytes(4, "big") if first else b"")
+        cap = FIRST_COMPACT_SHARE_CONTENT_SIZE if first else CONTINUATION_COMPACT_SHARE_CONTENT_SIZE
+        data_start = len(header) + 4
+        lo, hi = pos, pos + cap
+        first_unit = next((st for st in starts if lo <= st < hi), None)
+        reserved = 0 if first_unit is None else data_start + (first_unit - lo)
+        share = header + reserved.to_bytes(4, "big") + seq[lo:hi]
+        out.append(share + bytes(SHARE - len(share)))
+        pos = hi
+    return out
+
+
+def sparse_shares(ns, data, share_version=appconsts.SHARE_VERSION_ZERO):
+    """SparseShareSplitter.Write: ns ‖ info ‖ [sequence length] ‖ data ‖ zeros (shares.md:31-60)."""
+    out, pos = [], 0
+    for s in range(sparse_shares_needed(len(data))):
+        first = s == 0
+        header = ns + bytes([(share_version << 1) | (1 if first else 0)])
+        if first:
+            header += len(data).to_bytes(4, "big")
+        share = header + data[pos:pos + SHARE - len(header)]
+        out.append(share + bytes(SHARE - len(share)))
+        pos += SHARE - len(header)
+    return out
+
+
+def padding_share(ns):
+    """Namespace / reserved / tail padding share: ns ‖ info(first) ‖ sequence length 0 ‖ zeros (shares.md:82-122)."""
+    share = ns + b"\x01" + bytes(4)
+    return share + bytes(SHARE - len(share))
+
+
+# ---- square.Construct ----------------------------------------------------------------------------
+def construct(txs, max_square_size=appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND,
+              subtree_root_threshold=appconsts.SUBTREE_ROOT_THRESHOLD, square_size_upper_bound=None):
+    """square.Construct(txs, maxSquareSize, subtreeRootThreshold) -> (square size k, k*k shares, layout info).
+
+    square_size_upper_bound sizes the PFB share-index reservation (defaults to max_square_size).
+    """
+    upper = square_size_upper_bound or max_square_size
+    normal, pfbs, blobs = [], [], []
+    for raw in txs:
+        bt = unmarshal_blob_tx(raw)
+        if bt is None:
+            normal.append(raw)
+            continue
+        tx, bl = bt
+        pfbs.append({"tx": tx, "idx": [0] * len(bl)})
+        for j, b in enumerate(bl):
+            n = sparse_shares_needed(len(b["data"]))
+            blobs.append({"blob": b, "pfb": len(pfbs) - 1, "j": j, "n": n,
+                          "max_pad": sub_tree_width(n, subtree_root_threshold) - 1})
+    tx_seq = sum(len(varint(len(t))) + len(t) for t in normal)
+    worst = upper * upper
+    pfb_seq = sum(len(varint(len(w))) + len(w)
+                  for w in (marshal_index_wrapper(p["tx"], [worst] * len(p["idx"])) for p in pfbs))
+    tx_shares, pfb_reserved = compact_shares_needed(tx_seq), compact_shares_needed(pfb_seq)
+    current = tx_shares + pfb_reserved + sum(b["n"] + b["max_pad"] for b in blobs)
+    ss = 1
+    while ss * ss < max(current, 1):
+        ss <<= 1
+    if ss > max_square_size:
+        raise SquareError(f"square size {ss} exceeds the maximum {max_square_size}")
+    blobs.sort(key=lambda b: b["blob"]["ns"])  # stable: PFB order within a namespace
+    non_reserved_start = tx_shares + pfb_reserved
+    cursor = end_last = non_reserved_start
+    blob_out = []
+    for i, b in enumerate(blobs):
+        cursor = next_share_index(cursor, b["n"], subtree_root_threshold)
+        if i == 0:
+            non_reserved_start = cursor
+        pad = cursor - end_last
+        if pad > b["max_pad"]:
+            raise SquareError("blob padding exceeds its subtree width")
+        pfbs[b["pfb"]]["idx"][b["j"]] = cursor
+        if i > 0:
+            blob_out += [padding_share(blobs[i - 1]["blob"]["ns"])] * pad
+        blob_out += sparse_shares(b["blob"]["ns"], b["blob"]["data"], b["blob"]["share_version"])
+        cursor += b["n"]
+        end_last = cursor
+    square = compact_shares(TX_NAMESPACE, normal)
+    pfb_sh = compact_shares(PAY_FOR_BLOB_NAMESPACE, [marshal_index_wrapper(p["tx"], p["idx"]) for p in pfbs])
+    if len(pfb_sh) > pfb_reserved:
+        raise SquareError("PFB shares exceed their reservation")
+    square += pfb_sh
+    if blob_out:
+        square += [padding_share(PRIMARY_RESERVED_PADDING_NAMESPACE)] * (non_reserved_start - len(square))
+        square += blob_out
+    square += [padding_share(TAIL_PADDING_NAMESPACE)] * (ss * ss - len(square))
+    info = {"normal_txs": len(normal), "pfbs": len(pfbs), "blobs": len(blobs), "tx_shares": tx_shares,
+            "pfb_shares": len(pfb_sh), "pfb_reserved": pfb_reserved,
+            "first_blob": non_reserved_start if blobs else None, "current_size": current,
+            "pfb_share_indexes": [p["idx"] for p in pfbs]}
+    return ss, square, info
