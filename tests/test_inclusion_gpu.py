@@ -155,3 +155,28 @@ def test_dah_proto_round_trip(ctx):
         assert back.row_roots == d.row_roots and back.column_roots == d.column_roots and back.hash() == d.hash()
     with pytest.raises(da.DAError):
         da.data_availability_header_from_proto(da.DataAvailabilityHeader([bytes(90)], [bytes(90)]).to_proto())
+
+
+def test_max_square_nodes_and_proof_k128(ctx):
+    """Production maximum (k=128, SquareSizeUpperBound): exported nodes of sampled trees and a proof spanning rows."""
+    k = 128
+    ods = O.gen_ods(k, 0x128)
+    out = ctx.extend_commit_nodes(ods, want_eds=True)
+    eds = out["eds"]
+    for axis, key in ((0, "row_nodes"), (1, "col_nodes")):
+        for t in (0, 127, 128, 255):
+            assert np.array_equal(out[key][t], O.tree_levels(O.axis_leaf_nodes(eds, axis, t))), (axis, t)
+    p = ctx.share_inclusion_proof(ods, 1000, 1500)
+    assert p["data_root"] == out["dah"] and len(p["rows"]) == (1499 // k) - (1000 // k) + 1
+    for i, row in enumerate(p["rows"]):
+        r = p["start_row"] + i
+        assert row["nodes"] == O.nmt_prove_range(O.axis_leaf_nodes(eds, 0, r), row["start"], row["end"])
+
+
+def test_blob_commitment_largest_blob(ctx):
+    """An ~8 MB blob (16 Ki shares: SubTreeWidth 128, 128 mountains) and a tiny one in one call."""
+    rng = np.random.default_rng(8)
+    datas = [rng.integers(0, 256, 16384 * 482 - 4, dtype=np.uint8).tobytes(), b"\x07"]
+    ns = [bytes(19) + bytes(range(10)), bytes(19) + bytes(range(1, 11))]
+    got = ctx.blob_commitments(ns, datas, None, 64)
+    assert got == [O.blob_commitment(n, d)[1] for n, d in zip(ns, datas)]
