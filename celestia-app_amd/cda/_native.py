@@ -292,12 +292,17 @@ class Context:
         offs = np.zeros(nb + 1, np.uint64)
         offs[1:] = np.cumsum([len(d) for d in datas])
         sv = None if share_versions is None else np.ascontiguousarray(share_versions, np.uint8)
+        return [bytes(o) for o in self.blob_commitments_packed(ns, data, offs, sv, subtree_root_threshold)]
+
+    def blob_commitments_packed(self, namespaces, data, offsets, share_versions=None, subtree_root_threshold=64):
+        """cda_blob_commitments on pre-packed arrays: namespaces (n*29,) uint8, data uint8, offsets (n+1,) uint64."""
+        nb = len(offsets) - 1
         out = np.empty((nb, 32), np.uint8)
         err = ErrInfo()
-        rc = lib().cda_blob_commitments(self._h, nb, _p(ns), _p(data), _p(offs), _p(sv), subtree_root_threshold,
-                                        _p(out), ctypes.byref(err))
+        rc = lib().cda_blob_commitments(self._h, nb, _p(namespaces), _p(data), _p(offsets), _p(share_versions),
+                                        subtree_root_threshold, _p(out), ctypes.byref(err))
         _check(rc, err, self)
-        return [bytes(o) for o in out]
+        return out
 
     def merkle_roots(self, sets):
         """merkle.HashFromByteSlices of each list of 90-byte NMT nodes."""

@@ -19,6 +19,9 @@ struct cda_ctx {
   // another's hashing (no dependency between blocks).
   static constexpr int kMaxSub = 8;
   int nsub = 1;
+  // CDA_PIPELINE: chunks of a batch software-pipelined over two streams (RS of chunk i+1
+  // overlaps the hashing of chunk i); 1 = off.
+  int pipe_chunks = 1;
   hipStream_t sub[kMaxSub] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::string last_err;

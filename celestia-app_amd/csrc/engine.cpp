@@ -219,6 +219,35 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (rc) return rc;
   rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
   if (rc) return rc;
+  if (!c->prof && c->pipe_chunks > 1 && nblocks > 1) {
+    // Two-stream software pipeline: stream sub[0] runs the RS phase chunk after chunk,
+    // stream sub[1] hashes chunk i as soon as its RS phase is done, so the memory-bound
+    // RS of chunk i+1 overlaps the VALU-bound hashing of chunk i.
+    const uint32_t C = std::min<uint32_t>((uint32_t)c->pipe_chunks, nblocks);
+    hipStream_t srs = c->sub[0], ssha = c->sub[1];
+    if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
+        !dev_ok(c, hipStreamWaitEvent(srs, c->fork_ev, 0), "hipStreamWaitEvent") ||
+        !dev_ok(c, hipStreamWaitEvent(ssha, c->fork_ev, 0), "hipStreamWaitEvent"))
+      return CDA_E_DEVICE;
+    uint32_t done = 0;
+    for (uint32_t i = 0; i < C; i++) {
+      const uint32_t nb = (nblocks - done) / (C - i);
+      const uint8_t* o = d_ods + (size_t)done * k * k * CDA_SHARE;
+      uint8_t* e = d_eds + (size_t)done * w * w * CDA_SHARE;
+      if (int rc2 = enqueue_rs(c, k, nb, o, e, srs)) return rc2;
+      if (!dev_ok(c, hipEventRecord(c->join_ev[0], srs), "hipEventRecord") ||
+          !dev_ok(c, hipStreamWaitEvent(ssha, c->join_ev[0], 0), "hipStreamWaitEvent"))
+        return CDA_E_DEVICE;
+      if (int rc2 = enqueue_commit(c, k, nb, e, (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES,
+                                   (uint8_t*)d_dah + (size_t)done * 32, d_status + done, ssha, (size_t)done * w * w))
+        return rc2;
+      done += nb;
+    }
+    if (!dev_ok(c, hipEventRecord(c->join_ev[1], ssha), "hipEventRecord") ||
+        !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[1], 0), "hipStreamWaitEvent"))
+      return CDA_E_DEVICE;
+    return CDA_OK;
+  }
   const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
   if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
   if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
@@ -273,6 +302,7 @@ int cda_init(int device, cda_ctx** out) {
     return CDA_E_DEVICE;
   }
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
+  if (const char* e = getenv("CDA_PIPELINE")) c->pipe_chunks = std::max(1, std::min(64, atoi(e)));
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
     ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
