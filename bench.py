@@ -173,6 +173,28 @@ def pmc_traffic(kernel, B):
             "source": f"{os.path.relpath(files[-1], ROOT)} ({PMC_NAMES[kernel]}, B=128 profile scaled to B={B})"}
 
 
+def host_path_measure(ctx, k, nblocks=16, reps=3):
+    """The drop-in boundary with host buffers (cgo passes Go slices): cda_extend_commit_batch on nblocks host ODS,
+    with and without the EDS copy-out. PCIe-inclusive; reported beside, never as, the bench value."""
+    ods = np.stack([gen_ods(k, 0xC0FFEE + b) for b in range(min(4, nblocks))])
+    ods = np.ascontiguousarray(np.concatenate([ods] * (nblocks // len(ods)))).reshape(nblocks, k * k, 512)
+    out = {}
+    eds = np.ones((nblocks, 4 * k * k, 512), np.uint8)  # reused, already-touched output (a Go slice is zeroed)
+    for want_eds in (True, False):
+        ctx.extend_commit_batch(ods, want_eds=want_eds, eds_out=eds if want_eds else None)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ctx.extend_commit_batch(ods, want_eds=want_eds, eds_out=eds if want_eds else None)
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        out["with_eds" if want_eds else "roots_only"] = {"blocks_per_s": round(nblocks / best, 1),
+                                                         "ms": round(best * 1e3, 2)}
+    out["note"] = (f"{nblocks} k={k} blocks per call, pageable host memory (output reused), PCIe-inclusive: "
+                   "8 MiB in + 32 MiB EDS out per block")
+    return out
+
+
 def commitments_measure(ctx, nblobs=256, size=64 * 1024, reps=5):
     """x/blob share commitments (inclusion.CreateCommitments) of a batch of random blobs: one cda_blob_commitments
     call on pre-packed host arrays (H2D of the blob data included), next to the C oracle on one host thread."""
@@ -341,6 +363,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["repair_c4"] = repair_measure(ctx)
         result["blob_commitments"] = commitments_measure(ctx)
+        result["host_buffers"] = host_path_measure(ctx, k)
         result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -189,12 +189,12 @@ class Context:
         _check(rc, err, self)
         return eds, rr, cr, dah.tobytes()
 
-    def extend_commit_batch(self, ods, want_eds=True):
-        """ods: (nblocks, k*k, 512)."""
+    def extend_commit_batch(self, ods, want_eds=True, eds_out=None):
+        """ods: (nblocks, k*k, 512); eds_out: optional preallocated (nblocks, 4k^2, 512) uint8 output."""
         ods = np.ascontiguousarray(ods, np.uint8)
         nb, kk, L = ods.shape
         k = int(round(kk ** 0.5))
-        eds = np.empty((nb, 4 * k * k, L), np.uint8) if want_eds else None
+        eds = eds_out if eds_out is not None else (np.empty((nb, 4 * k * k, L), np.uint8) if want_eds else None)
         rr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
         cr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
         dah = np.empty((nb, 32), np.uint8)
