@@ -173,6 +173,22 @@ def pmc_traffic(kernel, B):
             "source": f"{os.path.relpath(files[-1], ROOT)} ({PMC_NAMES[kernel]}, B=128 profile scaled to B={B})"}
 
 
+def proof_measure(ctx, k, reps=3):
+    """pkg/proof NewShareInclusionProof for a 500-share range of a k=128 square (cda_share_inclusion_proof:
+    extension + node export + proof assembly, host ODS in)."""
+    ods = gen_ods(k, 0xC0FFEE)
+    ctx.share_inclusion_proof(ods, 1000, 1500)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = ctx.share_inclusion_proof(ods, 1000, 1500)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    return {"k": k, "shares": 500, "rows": len(out["rows"]), "ms": round(best * 1e3, 2),
+            "note": "one cda_share_inclusion_proof call: H2D of the ODS, extension, every tree node copied out, "
+                    "NMT range proofs + RFC-6962 aunts assembled from exported nodes"}
+
+
 def host_path_measure(ctx, k, nblocks=16, reps=3):
     """The drop-in boundary with host buffers (cgo passes Go slices): cda_extend_commit_batch on nblocks host ODS,
     with and without the EDS copy-out. PCIe-inclusive; reported beside, never as, the bench value."""
@@ -364,6 +380,7 @@ def main():
         result["repair_c4"] = repair_measure(ctx)
         result["blob_commitments"] = commitments_measure(ctx)
         result["host_buffers"] = host_path_measure(ctx, k)
+        result["share_proof"] = proof_measure(ctx, k)
         result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
