@@ -22,6 +22,8 @@ struct cda_ctx {
   // CDA_PIPELINE: chunks of a batch software-pipelined over two streams (RS of chunk i+1
   // overlaps the hashing of chunk i); 1 = off.
   int pipe_chunks = 1;
+  // CDA_CHUNK: blocks per sequential chunk on one stream (0 = whole batch at once)
+  int chunk_blocks = 0;
   hipStream_t sub[kMaxSub] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::string last_err;

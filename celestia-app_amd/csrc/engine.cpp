@@ -248,6 +248,20 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
       return CDA_E_DEVICE;
     return CDA_OK;
   }
+  if (c->chunk_blocks > 0 && (uint32_t)c->chunk_blocks < nblocks) {
+    // Sequential chunks on one stream: every phase of a chunk runs before the next chunk, so a chunk's
+    // working set (EDS + records) can stay in the 256 MB Infinity Cache between its phases.
+    for (uint32_t done = 0; done < nblocks;) {
+      const uint32_t nb = std::min<uint32_t>((uint32_t)c->chunk_blocks, nblocks - done);
+      if (int rc2 = enqueue_pipeline_one(c, k, nb, d_ods + (size_t)done * k * k * CDA_SHARE,
+                                         d_eds + (size_t)done * w * w * CDA_SHARE,
+                                         (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES,
+                                         (uint8_t*)d_dah + (size_t)done * 32, d_status + done, s, (size_t)done * w * w))
+        return rc2;
+      done += nb;
+    }
+    return CDA_OK;
+  }
   const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
   if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
   if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
@@ -303,6 +317,7 @@ int cda_init(int device, cda_ctx** out) {
   }
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
   if (const char* e = getenv("CDA_PIPELINE")) c->pipe_chunks = std::max(1, std::min(64, atoi(e)));
+  if (const char* e = getenv("CDA_CHUNK")) c->chunk_blocks = std::max(0, atoi(e));
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
     ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
