@@ -172,7 +172,8 @@ __device__ __forceinline__ void ld4(const uint4* p, uint32_t* w) {  // 4 x 16 B 
 }
 
 // Inner node from the two child records at pl / pr, written to po.  The
-// children are read block by block (through laundered pointers, so the reads
+// children are read block by block (through laundered pointers ordered after the
+// previous compression, so the reads
 // are not merged and kept live) and each compression is fenced: 111 VGPRs
 // instead of 205 for the version that held both children in registers.
 __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po) {
@@ -189,8 +190,8 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
   sha256_compress_fenced(st, m);
   {  // block 1: words 16..31 <- L words 15..22, R words 0..8
     uint32_t L[16], R[16];  // L words 12..27, R words 0..15
-    ld4(launder(pl) + 3, L);  // words 12..27: only 12..23 are read
-    ld4(launder(pr), R);      // words 0..15: only 0..11 are read
+    ld4(launder_after(pl, st[0]) + 3, L);  // words 12..27: only 12..23 are read
+    ld4(launder_after(pr, st[0]), R);      // words 0..15: only 0..11 are read
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int wi = 16 + i;
@@ -202,7 +203,7 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
   sha256_compress_fenced(st, m);
   {  // block 2: words 32..47 <- R words 8..23
     uint32_t R[16];
-    ld4(launder(pr) + 2, R);
+    ld4(launder_after(pr, st[0]) + 2, R);
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int wi = 32 + i;
@@ -216,8 +217,8 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
 
   // namespace range: min = L.min; max = R.min == parity ns ? L.max : R.max
   uint32_t L[16], R[16];
-  ld4(launder(pl), L);
-  ld4(launder(pr), R);
+  ld4(launder_after(pl, st[0]), L);
+  ld4(launder_after(pr, st[0]), R);
   bool rmin_max = true;
 #pragma unroll
   for (int i = 0; i < 7; i++) rmin_max &= (R[i] == 0xFFFFFFFFu);

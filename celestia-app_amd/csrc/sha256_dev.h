@@ -145,8 +145,10 @@ __device__ __forceinline__ void sha256_compress_n(uint32_t (&s)[N][8], uint32_t 
 
 // One compression with scheduling fences every 8 rounds and after the block.
 // Straight-line code with several compressions (NMT inner nodes: 3 blocks)
-// otherwise lets the machine scheduler hoist later message-schedule words and
-// loads far ahead: 205 VGPRs (2 waves/SIMD) for the node kernel, 111 with fences.
+// otherwise lets the machine scheduler hoist later message-schedule words far
+// ahead.  The fences alone do not stop IR-level passes from hoisting the child
+// loads of later blocks to the top (150 VGPRs, 3 waves/SIMD); launder_after()
+// below ties each load to the previous compression: 89 VGPRs, 5 waves/SIMD.
 __device__ __forceinline__ void sha256_compress_fenced(uint32_t s[8], const uint32_t w[16]) {
   uint32_t S[1][8], W[1][16];
 #pragma unroll
@@ -164,6 +166,13 @@ __device__ __forceinline__ void sha256_compress_fenced(uint32_t s[8], const uint
 template <typename T>
 __device__ __forceinline__ const T* launder(const T* p) {
   asm volatile("" : "+v"(p));
+  return p;
+}
+// launder(p) that also depends on `after`: loads through the result cannot be
+// hoisted above the computation of `after` (e.g. the previous compression).
+template <typename T>
+__device__ __forceinline__ const T* launder_after(const T* p, uint32_t after) {
+  asm volatile("" : "+v"(p) : "v"(after));
   return p;
 }
 
