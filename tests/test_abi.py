@@ -59,3 +59,15 @@ def test_wrapper_push_errors_without_gpu():
     t.push(b"\x01" * 512)
     with pytest.raises(PushError):
         t.push(b"\x00" * 512)
+
+
+def test_new_entry_points_reject_null_context_without_gpu():
+    # argument checks run before any device work (include/cda.h contract: negative codes, no abort)
+    L = cda.lib()
+    assert L.cda_blob_commitments(None, 1, None, None, None, None, 64, None, None) == N.E_ARG
+    assert L.cda_merkle_roots(None, 1, None, None, 90, None) == N.E_ARG
+    assert L.cda_extend_commit_nodes(None, 4, 512, None, None, None, None, None, None, None, None, None) == N.E_ARG
+    assert L.cda_share_inclusion_proof(None, 4, 512, None, 0, 1, None, None, None, None, None, None, None, None,
+                                       None, None) == N.E_ARG
+    assert N.strerror(N.E_BLOB_SIZE) == "cannot use zero blob size"
+    assert N.strerror(N.E_SHARE_VERSION) == "unsupported share version"
