@@ -331,3 +331,17 @@ def test_rsmt2d_repair_api(ctx):
     sq2 = rsmt2d.import_extended_data_square([None] * (4 * k * k), rsmt2d.LeoRSCodec(ctx))
     with pytest.raises(rsmt2d.ErrUnrepairableDataSquare):
         sq2.repair([bytes(r) for r in rr], [bytes(c) for c in cr])
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128, 256])
+def test_extend_commit_matches_committed_digests(ctx, k):
+    """Device EDS / roots / DAH against the committed oracle digests (tests/golden/oracle_digests.json)."""
+    import hashlib
+    import json
+    import os
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                     "oracle_digests.json")))[str(k)]
+    eds, rr, cr, dah = ctx.extend_commit(O.gen_ods(k, fx["seed"]))
+    assert dah.hex() == fx["dah"]
+    assert hashlib.sha256(eds.tobytes()).hexdigest() == fx["eds_sha256"]
+    assert hashlib.sha256(rr.tobytes() + cr.tobytes()).hexdigest() == fx["roots_sha256"]

@@ -205,3 +205,17 @@ def test_oracle_reproduces_mainnet_block_408_data_hash():
     # non-constant data: parity differs from the data it encodes
     e = eds.reshape(64, 64, 512)
     assert not np.array_equal(e[:32, 32:], e[:32, :32])
+
+
+def test_oracle_matches_committed_digests():
+    """Regression pin: the oracle's outputs on the seeded squares equal tests/golden/oracle_digests.json."""
+    import hashlib
+    import json
+    import os
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_digests.json")))
+    for ks in ("1", "8", "32", "64"):
+        k = int(ks)
+        rc, eds, rr, cr, dah = O.extend_commit(O.gen_ods(k, fx[ks]["seed"]))
+        assert rc == 0 and dah.hex() == fx[ks]["dah"]
+        assert hashlib.sha256(eds.tobytes()).hexdigest() == fx[ks]["eds_sha256"]
+        assert hashlib.sha256(rr.tobytes() + cr.tobytes()).hexdigest() == fx[ks]["roots_sha256"]
