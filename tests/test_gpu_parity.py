@@ -345,3 +345,31 @@ def test_extend_commit_matches_committed_digests(ctx, k):
     assert dah.hex() == fx["dah"]
     assert hashlib.sha256(eds.tobytes()).hexdigest() == fx["eds_sha256"]
     assert hashlib.sha256(rr.tobytes() + cr.tobytes()).hexdigest() == fx["roots_sha256"]
+
+
+def test_concurrent_calls_on_one_context(ctx):
+    """rsmt2d calls Codec.Encode / tree Root concurrently from per-axis goroutines (SURVEY.md §8b Threading):
+    the ctx mutex keeps concurrent callers correct."""
+    import threading
+    rng = np.random.default_rng(21)
+    jobs = [rng.integers(0, 256, (k, 512), dtype=np.uint8) for k in (16, 64, 128, 32, 8, 100)]
+    want = [O.leo_encode(d) for d in jobs]
+    ods = O.gen_ods(16, 77)
+    rc, _, rr_o, _, dah_o = O.extend_commit(ods)
+    errors = []
+
+    def worker(i):
+        try:
+            for _ in range(3):
+                assert np.array_equal(ctx.rs_encode(jobs[i]), want[i])
+                _, rr, _, dah = ctx.extend_commit(ods)
+                assert np.array_equal(rr, rr_o) and dah == dah_o
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(len(jobs))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not errors, errors
