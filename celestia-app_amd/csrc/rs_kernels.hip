@@ -36,25 +36,39 @@ __constant__ unsigned long long c_col8[256];
 // 8 words (32 bytes, little-endian) <-> 8 planes; plane j bit (8b+i) = bit j of
 // byte 4i+b.  Three SWAPMOVE stages transpose the 8x8 bit blocks of each byte
 // lane; the transform is an involution.
-__device__ __forceinline__ void swapmove(uint32_t& a, uint32_t& b, uint32_t mask, int n) {
-  uint32_t t = __builtin_amdgcn_bitop3_b32(a >> n, b, mask, 0x28);  // ((a>>n) ^ b) & mask
-  b ^= t;
-  a ^= t << n;
+//
+// Each SWAPMOVE is two shifts and two v_bitop3 selects (b' = m ? a>>n : b,
+// a' = m<<n ? b<<n : a).  The six masks are held in VGPRs (SliceMasks): a VALU op
+// reading an SGPR or literal issues at half rate on gfx950 (tools/valu_ubench.hip),
+// and the compiler otherwise keeps the mask constants in SGPRs.
+struct SliceMasks {
+  uint32_t m1, m1h, m2, m2h, m4, m4h;
+};
+__device__ __forceinline__ SliceMasks slice_masks() {
+  SliceMasks k{0x55555555u, 0xAAAAAAAAu, 0x33333333u, 0xCCCCCCCCu, 0x0F0F0F0Fu, 0xF0F0F0F0u};
+  asm volatile("" : "+v"(k.m1), "+v"(k.m1h), "+v"(k.m2), "+v"(k.m2h), "+v"(k.m4), "+v"(k.m4h));
+  return k;
 }
-__device__ __forceinline__ void bitslice8(uint32_t w[8]) {
-  swapmove(w[0], w[1], 0x55555555u, 1);
-  swapmove(w[2], w[3], 0x55555555u, 1);
-  swapmove(w[4], w[5], 0x55555555u, 1);
-  swapmove(w[6], w[7], 0x55555555u, 1);
-  swapmove(w[0], w[2], 0x33333333u, 2);
-  swapmove(w[1], w[3], 0x33333333u, 2);
-  swapmove(w[4], w[6], 0x33333333u, 2);
-  swapmove(w[5], w[7], 0x33333333u, 2);
-  swapmove(w[0], w[4], 0x0F0F0F0Fu, 4);
-  swapmove(w[1], w[5], 0x0F0F0F0Fu, 4);
-  swapmove(w[2], w[6], 0x0F0F0F0Fu, 4);
-  swapmove(w[3], w[7], 0x0F0F0F0Fu, 4);
+__device__ __forceinline__ void swapmove(uint32_t& a, uint32_t& b, uint32_t m, uint32_t mh, int n) {
+  const uint32_t nb = __builtin_amdgcn_bitop3_b32(m, a >> n, b, 0xCA);
+  a = __builtin_amdgcn_bitop3_b32(mh, b << n, a, 0xCA);
+  b = nb;
 }
+__device__ __forceinline__ void bitslice8(uint32_t w[8], const SliceMasks& k) {
+  swapmove(w[0], w[1], k.m1, k.m1h, 1);
+  swapmove(w[2], w[3], k.m1, k.m1h, 1);
+  swapmove(w[4], w[5], k.m1, k.m1h, 1);
+  swapmove(w[6], w[7], k.m1, k.m1h, 1);
+  swapmove(w[0], w[2], k.m2, k.m2h, 2);
+  swapmove(w[1], w[3], k.m2, k.m2h, 2);
+  swapmove(w[4], w[6], k.m2, k.m2h, 2);
+  swapmove(w[5], w[7], k.m2, k.m2h, 2);
+  swapmove(w[0], w[4], k.m4, k.m4h, 4);
+  swapmove(w[1], w[5], k.m4, k.m4h, 4);
+  swapmove(w[2], w[6], k.m4, k.m4h, 4);
+  swapmove(w[3], w[7], k.m4, k.m4h, 4);
+}
+__device__ __forceinline__ void bitslice8(uint32_t w[8]) { bitslice8(w, slice_masks()); }
 
 // x ^= M * y, M(j,b) = bit (8b+j) of cb
 __device__ __forceinline__ void gf8_muladd(uint32_t x[8], const uint32_t y[8], unsigned long long cb) {
@@ -336,6 +350,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
   uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
 
   uint32_t E[8][8];
+  const SliceMasks km = slice_masks();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int x = x2_of(w, sw, r, 1);
@@ -349,7 +364,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
       }
       E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
       E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
-      bitslice8(E[r]);
+      bitslice8(E[r], km);
       apply8(E[r], kPhi8);  // Cantor coordinates -> standard basis
     } else {
 #pragma unroll
@@ -372,6 +387,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
 #pragma unroll
   for (int d = (F2 - 1 < 3 ? F2 - 1 : 3); d >= 1; d--) layer2_u<false, M>(E, w, 1, d);
   layer2_d0<false, M>(E, w, 1, upper);
+  const SliceMasks ko = slice_masks();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int x = x2_of(w, sw, r, 1);
@@ -380,7 +396,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
 #pragma unroll
       for (int j = 0; j < 8; j++) v[j] = E[r][j];
       apply8(v, kPhiInv8);  // standard basis -> Cantor coordinates
-      bitslice8(v);
+      bitslice8(v, ko);
       uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
       q[0] = make_uint4(v[0], v[1], v[2], v[3]);
       q[1] = make_uint4(v[4], v[5], v[6], v[7]);
