@@ -23,29 +23,10 @@
 #include <vector>
 
 #include "cda_internal.h"
+#include "gf_slice.h"
 
 namespace cda {
 namespace dec {
-
-__device__ __forceinline__ void swapmove(uint32_t& a, uint32_t& b, uint32_t mask, int n) {
-  uint32_t t = __builtin_amdgcn_bitop3_b32(a >> n, b, mask, 0x28);
-  b ^= t;
-  a ^= t << n;
-}
-__device__ __forceinline__ void bitslice8(uint32_t* w) {
-  swapmove(w[0], w[1], 0x55555555u, 1);
-  swapmove(w[2], w[3], 0x55555555u, 1);
-  swapmove(w[4], w[5], 0x55555555u, 1);
-  swapmove(w[6], w[7], 0x55555555u, 1);
-  swapmove(w[0], w[2], 0x33333333u, 2);
-  swapmove(w[1], w[3], 0x33333333u, 2);
-  swapmove(w[4], w[6], 0x33333333u, 2);
-  swapmove(w[5], w[7], 0x33333333u, 2);
-  swapmove(w[0], w[4], 0x0F0F0F0Fu, 4);
-  swapmove(w[1], w[5], 0x0F0F0F0Fu, 4);
-  swapmove(w[2], w[6], 0x0F0F0F0Fu, 4);
-  swapmove(w[3], w[7], 0x0F0F0F0Fu, 4);
-}
 
 template <int PL>
 struct Field;

@@ -26,49 +26,12 @@
 
 #include "cda_internal.h"
 #include "gf8_mul_asm.h"
+#include "gf_slice.h"
 
 namespace cda {
 
 __constant__ uint16_t c_skew8[256];
 __constant__ unsigned long long c_col8[256];
-
-// --- bit slicing -----------------------------------------------------------
-// 8 words (32 bytes, little-endian) <-> 8 planes; plane j bit (8b+i) = bit j of
-// byte 4i+b.  Three SWAPMOVE stages transpose the 8x8 bit blocks of each byte
-// lane; the transform is an involution.
-//
-// Each SWAPMOVE is two shifts and two v_bitop3 selects (b' = m ? a>>n : b,
-// a' = m<<n ? b<<n : a).  The six masks are held in VGPRs (SliceMasks): a VALU op
-// reading an SGPR or literal issues at half rate on gfx950 (tools/valu_ubench.hip),
-// and the compiler otherwise keeps the mask constants in SGPRs.
-struct SliceMasks {
-  uint32_t m1, m1h, m2, m2h, m4, m4h;
-};
-__device__ __forceinline__ SliceMasks slice_masks() {
-  SliceMasks k{0x55555555u, 0xAAAAAAAAu, 0x33333333u, 0xCCCCCCCCu, 0x0F0F0F0Fu, 0xF0F0F0F0u};
-  asm volatile("" : "+v"(k.m1), "+v"(k.m1h), "+v"(k.m2), "+v"(k.m2h), "+v"(k.m4), "+v"(k.m4h));
-  return k;
-}
-__device__ __forceinline__ void swapmove(uint32_t& a, uint32_t& b, uint32_t m, uint32_t mh, int n) {
-  const uint32_t nb = __builtin_amdgcn_bitop3_b32(m, a >> n, b, 0xCA);
-  a = __builtin_amdgcn_bitop3_b32(mh, b << n, a, 0xCA);
-  b = nb;
-}
-__device__ __forceinline__ void bitslice8(uint32_t w[8], const SliceMasks& k) {
-  swapmove(w[0], w[1], k.m1, k.m1h, 1);
-  swapmove(w[2], w[3], k.m1, k.m1h, 1);
-  swapmove(w[4], w[5], k.m1, k.m1h, 1);
-  swapmove(w[6], w[7], k.m1, k.m1h, 1);
-  swapmove(w[0], w[2], k.m2, k.m2h, 2);
-  swapmove(w[1], w[3], k.m2, k.m2h, 2);
-  swapmove(w[4], w[6], k.m2, k.m2h, 2);
-  swapmove(w[5], w[7], k.m2, k.m2h, 2);
-  swapmove(w[0], w[4], k.m4, k.m4h, 4);
-  swapmove(w[1], w[5], k.m4, k.m4h, 4);
-  swapmove(w[2], w[6], k.m4, k.m4h, 4);
-  swapmove(w[3], w[7], k.m4, k.m4h, 4);
-}
-__device__ __forceinline__ void bitslice8(uint32_t w[8]) { bitslice8(w, slice_masks()); }
 
 // x ^= M * y, M(j,b) = bit (8b+j) of cb
 __device__ __forceinline__ void gf8_muladd(uint32_t x[8], const uint32_t y[8], unsigned long long cb) {
@@ -204,21 +167,41 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
 // tools/valu_ubench.hip).
 __constant__ uint8_t c_cpoly8[256];  // per skew index: alpha^skew in std basis, 0 = no multiply
 
-constexpr uint8_t kPhi8[8] = {1, 214, 152, 146, 86, 200, 88, 230};     // columns: phi(1<<j)
-constexpr uint8_t kPhiInv8[8] = {1, 104, 92, 100, 114, 240, 86, 18};  // columns: phi^-1(1<<j)
+// phi columns (phi(1<<j)):    {1, 214, 152, 146, 86, 200, 88, 230}
+// phi^-1 columns:              {1, 104, 92, 100, 114, 240, 86, 18}
+// (to_std8 / to_cantor8 below apply them to 8 bit-planes.)
 
-__device__ __forceinline__ void apply8(uint32_t (&v)[8], const uint8_t (&cols)[8]) {
-  uint32_t o[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++)
-      if ((cols[j] >> i) & 1) acc ^= v[j];
-    o[i] = acc;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) v[i] = o[i];
+// The two basis changes of the g2 kernel as hand-scheduled XOR3 programs
+// (7 VALU each instead of 19 / 17 v_xor as a plain row-by-row XOR of the
+// matrices above); checked against the oracle by the GPU parity tests.
+__device__ __forceinline__ uint32_t xor3v(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ void to_std8(uint32_t (&v)[8]) {  // planes *= phi
+  const uint32_t t = xor3v(v[1], v[4], v[7]);
+  const uint32_t u = xor3v(v[1], v[2], v[3]);
+  const uint32_t o1 = t ^ v[3], o3 = xor3v(v[2], v[5], v[6]), o4 = xor3v(u, v[4], v[6]);
+  const uint32_t o6 = xor3v(t, v[5], v[6]), o7 = xor3v(u, v[5], v[7]), o5 = v[7];
+  v[1] = o1;
+  v[2] = t;
+  v[3] = o3;
+  v[4] = o4;
+  v[5] = o5;
+  v[6] = o6;
+  v[7] = o7;
+}
+__device__ __forceinline__ void to_cantor8(uint32_t (&v)[8]) {  // planes *= phi^-1
+  const uint32_t o1 = xor3v(v[4], v[6], v[7]), o2 = xor3v(v[2], v[3], v[6]), o3 = v[1] ^ v[2];
+  const uint32_t o4 = xor3v(o1, v[2], v[5]);
+  const uint32_t o5 = xor3v(v[1], v[3], v[4]) ^ v[5];
+  const uint32_t o6 = xor3v(o5, v[2], v[6]), o7 = v[5];
+  v[1] = o1;
+  v[2] = o2;
+  v[3] = o3;
+  v[4] = o4;
+  v[5] = o5;
+  v[6] = o6;
+  v[7] = o7;
 }
 
 // X ^= c * Y in the standard basis (c wave-uniform): gf8_muladd_asm, generated by
@@ -365,7 +348,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
       E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
       E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
       bitslice8(E[r], km);
-      apply8(E[r], kPhi8);  // Cantor coordinates -> standard basis
+      to_std8(E[r]);  // Cantor coordinates -> standard basis
     } else {
 #pragma unroll
       for (int j = 0; j < 8; j++) E[r][j] = 0;
@@ -395,7 +378,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
       uint32_t v[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) v[j] = E[r][j];
-      apply8(v, kPhiInv8);  // standard basis -> Cantor coordinates
+      to_cantor8(v);  // standard basis -> Cantor coordinates
       bitslice8(v, ko);
       uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
       q[0] = make_uint4(v[0], v[1], v[2], v[3]);
