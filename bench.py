@@ -98,32 +98,60 @@ def _host_cpu():
     return model, flags
 
 
-def cpu_baseline(k, min_seconds):
-    """The CPU restatement (oracle/, 'port') on this host: bounded samples of k-blocks, all-thread and 1-thread."""
+def _host_topology():
+    """nproc, the bench process's affinity, physical cores and the cgroup CPU quota of this host."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    phys = set()
+    try:
+        pid = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":", 1)[1].strip()
+                phys.add((pid, core))
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": aff, "physical_cores": len(phys) or None, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(k, seconds):
+    """The CPU restatement (oracle/, 'port') on this host's cores: whole single-threaded
+    ExtendShares+NewDataAvailabilityHeader calls on independent blocks, one worker per thread,
+    swept over 1 / 16 / 64 / all threads of the affinity mask (all = `cores`)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    threads = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1))
+    topo = _host_topology()
+    allt = topo["affinity"]
     ods = gen_ods(k, 0xC0FFEE)
-
-    def rate(nthreads, seconds):
-        n, t0 = 0, time.perf_counter()
-        while True:
-            rc, *_ = O.extend_commit(ods, want_eds=True, nthreads=nthreads)
-            assert rc == 0
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                return n, el
-
-    n, el = rate(threads, min_seconds)
-    n1, el1 = rate(1, max(2.0, min_seconds / 3))
+    counts = sorted({1, min(16, allt), min(64, allt), allt})
+    sweep, total_blocks = {}, {}
+    for n in counts:
+        blocks, el = O.extend_commit_throughput(ods, n, seconds / len(counts))
+        sweep[str(n)] = round(blocks / el, 2)
+        total_blocks[str(n)] = (blocks, round(el, 2))
     model, flags = _host_cpu()
-    return {"value": n / el, "unit": "blocks/s", "cores": threads, "kind": "port",
-            "single_thread_value": n1 / el1,
-            "host": {"cpu": model, "simd": flags, "os_cpus": os.cpu_count()},
-            "sample": f"{n} x k={k} ExtendShares+NewDataAvailabilityHeader via oracle/liboracle.so "
-                      f"(C restatement, OpenSSL SHA-256, AVX2 Leopard; not the Go reference), {threads} threads, "
-                      f"{el:.1f} s; 1 thread: {n1} blocks in {el1:.1f} s"}
+    best = max(sweep, key=lambda n: sweep[n])
+    phys = topo["physical_cores"] or allt
+    return {"value": sweep[best], "unit": "blocks/s", "cores": int(best), "kind": "port",
+            "single_thread_value": sweep["1"], "sweep_threads_blocks_per_s": sweep,
+            "all_threads": {"threads": allt, "value": sweep[str(allt)]},
+            "full_host_linear_extrapolation": {"cores": phys, "value": round(sweep["1"] * phys, 1),
+                                               "note": "single-thread rate x physical cores: an upper bound for "
+                                                       "the whole host, not a measurement (the bench process is "
+                                                       "limited by its cgroup CPU quota)"},
+            "host": dict(topo, cpu=model, simd=flags),
+            "sample": f"k={k} ExtendShares+NewDataAvailabilityHeader (EDS written) via oracle/liboracle.so "
+                      f"(C restatement, OpenSSL SHA-256 (SHA-NI), AVX2 Leopard; not the Go reference): independent "
+                      f"blocks, one single-threaded call per worker thread, {seconds / len(counts):.1f} s per thread "
+                      f"count over 1..{allt} threads of the affinity mask; value = the best count (the cgroup CPU "
+                      f"quota is {topo['cgroup_cpu_quota']} CPUs); (blocks, s) per count: {total_blocks}"}
 
 
 def repair_measure(ctx, k=128, survive=0.5, reps=3):
@@ -152,25 +180,38 @@ def repair_measure(ctx, k=128, survive=0.5, reps=3):
 
 
 # bench kernel name -> rocprofv3 kernel name in profiles/*_counters.json
-PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "nmt_level1": "nmt_level_kernel<true>", "dah": "dah_kernel"}
+PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "nmt_level1": "nmt_level_kernel<true>", "dah": "dah_kernel",
+             "rs_encode8_rows": "rs_encode8_g2_kernel<7>", "rs_encode8_cols": "rs_encode8_g2_kernel<7>"}
+PMC_BATCH = 128  # scripts/profile.sh profiles the default bench step (B = 128 blocks)
 
 
-def pmc_traffic(kernel, B):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary (profiles/r01_*_counters.json,
-    hbm_bytes_corrected = 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), measured on
-    this bench at B = 128 and scaled to the batch; None when no profile covers the kernel."""
+def pmc_counters(kernel, B):
+    """Per-launch PMC values of `kernel` from the newest committed rocprofv3 summary
+    (profiles/r0*_counters.json; scripts/profile.sh + scripts/summarize_prof.py), scaled from the
+    profiled batch to B.  hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (the gfx950 correction of
+    MI355X_MICROARCH.md); valu_insts = SQ_INSTS_VALU (wave-instructions).  None if not covered."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_*_counters.json")))
-    if not files or kernel not in PMC_NAMES:
+    if kernel not in PMC_NAMES:
         return None
-    try:
-        c = json.load(open(files[-1])).get(PMC_NAMES[kernel])
-    except (OSError, ValueError):
-        return None
-    if not c or "hbm_bytes_corrected" not in c:
-        return None
-    return {"bytes": int(c["hbm_bytes_corrected"] * B / 128),
-            "source": f"{os.path.relpath(files[-1], ROOT)} ({PMC_NAMES[kernel]}, B=128 profile scaled to B={B})"}
+    import re
+
+    def order(f):  # r<round>_v<version>_counters.json, newest last
+        m = re.match(r"r(\d+)(?:_v(\d+))?", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2) or 0)) if m else (0, 0)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_counters.json")), key=order)
+    for f in reversed(files):
+        try:
+            c = json.load(open(f)).get(PMC_NAMES[kernel])
+        except (OSError, ValueError):
+            continue
+        if not c:
+            continue
+        scale = B / float(c.get("bench_batch", PMC_BATCH))
+        return {"hbm_bytes": int(c["hbm_bytes_corrected"] * scale) if "hbm_bytes_corrected" in c else None,
+                "valu_insts": c["SQ_INSTS_VALU"] * scale if "SQ_INSTS_VALU" in c else None,
+                "source": f"{os.path.relpath(f, ROOT)} ({PMC_NAMES[kernel]}, B={c.get('bench_batch', PMC_BATCH)} "
+                          f"profile scaled to B={B})"}
+    return None
 
 
 def proof_measure(ctx, k, reps=3):
@@ -242,6 +283,70 @@ def commitments_measure(ctx, nblobs=256, size=64 * 1024, reps=5):
                     "oracle/inclusion.c on 1 thread (OpenSSL SHA-256), first results checked bit-exact"}
 
 
+def launch_ranks(args):
+    """bench.py --gpus N without torchrun: spawn N rank processes of this script (before anything
+    touches the GPU), one per device, rank r -> device r % device_count; exit with the worst rank's code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
+def dist_setup(world, local, dry_run):
+    """Device for this rank and the process group.  Ranks that share a device (a 1-GPU lease running
+    --gpus 2 as a logic check) or a dry run use gloo; one rank per device uses RCCL ("nccl")."""
+    import torch
+    import torch.distributed as dist
+    if dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return None, "gloo", False
+    ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+    if ndev < 1:
+        raise RuntimeError("no HIP device visible")
+    dev = torch.device("cuda", local % ndev)
+    torch.cuda.set_device(dev)
+    shared = world > ndev
+    backend = "gloo" if shared else "nccl"
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return dev, backend, shared
+
+
+def max_over_ranks(x, world, backend, dev):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world, backend, dev):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+VALU_CYCLES_PER_WAVE_INSTR = 2  # wave64 on a SIMD-32 (MI355X_MICROARCH.md, execution model)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,29 +355,40 @@ def main():
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--batch", type=int, default=128,
                     help="independent blocks per GPU per step (128 = config C3: 1024 blocks over 8 GPUs)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the repair/commitment/host-path/proof extras")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (spawn, process group, max-over-ranks); no GPU work")
     ap.add_argument("--workload", choices=["block_batch", "split"], default="block_batch",
                     help="block_batch: B independent blocks per GPU (default, BASELINE metric); "
                          "split: ONE k-square split over all ranks with an RCCL all-to-all (config C5, --k 512)")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     if args.workload == "split":
         return bench_split(args)
-
-    import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    dev, backend, shared = dist_setup(world, local, args.dry_run)
+    import torch
+    import torch.distributed as dist
+    if args.dry_run:
+        if world > 1:
+            dist.barrier()
+        ranks = sum_over_ranks(1.0, world, backend, dev)
+        t = max_over_ranks(float(rank), world, backend, dev)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(ranks), "max_rank": int(t),
+                              "backend": backend}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     import cda
-    ctx = cda.Context(local)
+    ctx = cda.Context(dev.index)
     k, B = args.k, args.batch
     w = 2 * k
     # synthetic, distinct blocks per rank (seed = 0xC0FFEE + global block index)
@@ -304,11 +420,7 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, backend, dev)
 
     blocks = world * B * args.steps
     value = blocks / elapsed
@@ -326,18 +438,34 @@ def main():
     kern = {n: {"avg_ms": ms / max(1, cnt), "launches": cnt, "total_ms": ms} for n, (ms, cnt) in prof.items()}
     dom = max(kern, key=lambda n: kern[n]["total_ms"])
     HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    clk = 2.4e9  # max engine clock, MI355X_MICROARCH.md
+    # VALU issue peak: every SIMD (4 per CU) issues one wave64 instruction per 2 cycles
+    valu_peak_tops = ncu * 4 * clk / VALU_CYCLES_PER_WAVE_INSTR * 64 / 1e12
     dom_step_bytes = kernel_step_bytes(dom, k, B)
-    dom_ms_per_step = kern[dom]["total_ms"] / prof_steps  # = launches/step x avg launch duration
-    achieved = dom_step_bytes / (dom_ms_per_step * 1e-3) / 1e9 if dom_step_bytes else None
+    launches_per_step = max(1, kern[dom]["launches"] // prof_steps)
+    dom_launch_bytes = dom_step_bytes // launches_per_step if dom_step_bytes else None
+    dom_avg_s = kern[dom]["avg_ms"] * 1e-3
+    hbm_gbs = dom_launch_bytes / dom_avg_s / 1e9 if dom_launch_bytes else None
+    pmc = pmc_counters(dom, B)
     path_gbs = block_bytes(k) * value / world / 1e9
-    # VALU view: SHA-256 compressions are the binding resource;
-    # ceiling = register-only sha256_compress throughput measured by tools/sha_ubench.hip.
     comp_per_s = block_compressions_engine(k) * value / world
-    SHA_CEIL = 28.6e9
-    sha_kernels = [n for n in kern if n in ("leaf_hash", "nmt_level1", "nmt_level")]
-    sha_ms = sum(kern[n]["total_ms"] for n in sha_kernels) / prof_steps
-    sha_comp_step = B * (block_compressions_engine(k) - 2 * (2 * (2 * k)) + 2)  # minus the DAH's
-    sha_rate = sha_comp_step / (sha_ms * 1e-3) if sha_ms else None
+
+    roofline = {"kernel": dom, "avg_launch_ms": round(kern[dom]["avg_ms"], 4), "bytes_per_launch": dom_launch_bytes,
+                "traffic": pmc["hbm_bytes"] if pmc else None}
+    if pmc and pmc.get("valu_insts"):
+        achieved = pmc["valu_insts"] * 64 / dom_avg_s / 1e12
+        roofline.update({"bound": "valu", "achieved": round(achieved, 2), "peak": round(valu_peak_tops, 2),
+                         "unit": "TOPS", "frac": round(achieved / valu_peak_tops, 4),
+                         "valu_wave_instr_per_launch": int(pmc["valu_insts"]),
+                         "peak_def": f"{ncu} CU x 4 SIMD x 2.4 GHz / 2 cycles per wave64 VALU instruction x 64 lanes "
+                                     "(int32 lane-ops/s)",
+                         "hbm": {"achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK, "unit": "GB/s",
+                                 "frac": round(hbm_gbs / HBM_PEAK, 4) if hbm_gbs else None},
+                         "counters_source": pmc["source"]})
+    else:  # no PMC pass covers this kernel: HBM view only
+        roofline.update({"bound": "hbm", "achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK,
+                         "unit": "GB/s", "frac": round(hbm_gbs / HBM_PEAK, 4) if hbm_gbs else None})
 
     result = {
         "metric": "ODS->EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s",
@@ -354,34 +482,24 @@ def main():
         "data": "synthetic (namespace-sorted random shares, SplitMix64 seed 0xC0FFEE+block)",
         "config": {"workload": f"k{k}_block_batch: da.ExtendShares+NewDataAvailabilityHeader on {B} independent "
                                f"k={k} blocks per GPU per step (configs[1] per block, batched as configs[2])",
-                   "k": k, "blocks_per_gpu_per_step": B, "share_size": 512, "parallelism": f"blocks x{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1) if achieved else None,
-                     "peak": HBM_PEAK, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK, 4) if achieved else None, "traffic": None,
-                     "bytes_per_launch": (dom_step_bytes // max(1, kern[dom]["launches"] // prof_steps))
-                     if dom_step_bytes else None,
-                     "avg_launch_ms": round(kern[dom]["avg_ms"], 4),
-                     "note": "traffic: PMC HBM bytes per launch are in profiles/r01_*_counters.json "
-                             "(rocprofv3 pass, FETCH_SIZE x2 + WRITE_SIZE); the SHA kernels are VALU-bound, "
-                             "see valu_roofline"},
-        "valu_roofline": {"kernels": sha_kernels, "achieved": sha_rate, "peak": SHA_CEIL,
-                          "unit": "SHA-256 compressions/s",
-                          "frac": round(sha_rate / SHA_CEIL, 4) if sha_rate else None,
-                          "peak_source": "tools/sha_ubench.hip register-only sha256_compress on MI355X"},
+                   "k": k, "blocks_per_gpu_per_step": B, "share_size": 512,
+                   "parallelism": f"blocks x{world}" + (" (ranks share one device, gloo)" if shared else "")},
+        "roofline": roofline,
         "path_hbm_gbs": round(path_gbs, 1),
         "sha256_compressions_per_s": comp_per_s,
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
-    traffic = pmc_traffic(dom, B)
-    if traffic:
-        result["roofline"]["traffic"] = traffic["bytes"]
-        result["roofline"]["traffic_source"] = traffic["source"]
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_extras:
         result["repair_c4"] = repair_measure(ctx)
         result["blob_commitments"] = commitments_measure(ctx)
         result["host_buffers"] = host_path_measure(ctx, k)
         result["share_proof"] = proof_measure(ctx, k)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
+        cb = result["cpu_baseline"]
+        result["gpu_vs_cpu"] = {"measured_best": round(value / cb["value"], 1),
+                                "full_host_linear_extrapolation": round(
+                                    value / cb["full_host_linear_extrapolation"]["value"], 1)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
@@ -396,13 +514,10 @@ def bench_split(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    dev, backend, shared = dist_setup(world, local, False)
     import cda
     from cda import split
-    ctx = cda.Context(local)
+    ctx = cda.Context(dev.index)
     ops = split.DeviceOps(ctx)
     k = args.k
     (r0, r1), _ = split.plan(k, world, rank)
@@ -419,11 +534,7 @@ def bench_split(args):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, backend, dev)
     value = args.steps / elapsed
     result = {
         "metric": f"ODS->EDS+DAH squares/sec, one k={k} square split over {world} GPU(s)",

@@ -14,12 +14,14 @@
  * SHA-256 is OpenSSL's (SHA-NI on x86 hosts) — the same primitive as Go's
  * crypto/sha256 used through consts.NewBaseHashFunc (global_consts.go:86).
  */
+#define _POSIX_C_SOURCE 200809L
 #include <math.h>
 #include <openssl/sha.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "oracle.h"
 
@@ -329,6 +331,77 @@ int ora_extend_commit(int count, size_t share_len, const uint8_t* shares, uint8_
   if (rc == ORA_OK) ora_dah_hash(2 * k, row_roots, col_roots, dah);
   if (!eds_or_null) free(eds);
   return rc;
+}
+
+/* ------------------------------------------------------------------ */
+/* Throughput sample for the bench's cpu_baseline: `nthreads` workers  */
+/* each run whole ExtendShares+NewDataAvailabilityHeader calls (one    */
+/* block per call, single-threaded inside) on the same ODS until       */
+/* `seconds` have passed — independent blocks spread over every core,  */
+/* the CPU analogue of the GPU batch.  Returns blocks completed; the   */
+/* wall time until the last worker finished goes to *elapsed.          */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  int count;
+  size_t L;
+  const uint8_t* ods;
+  double deadline;
+  atomic_long done;
+  atomic_int rc;
+  uint8_t dah0[32];
+} tput_t;
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void* tput_worker(void* p) {
+  tput_t* t = (tput_t*)p;
+  const int k = (int)lround(sqrt((double)t->count));
+  uint8_t* eds = (uint8_t*)malloc((size_t)4 * t->count * t->L);
+  uint8_t* rr = (uint8_t*)malloc((size_t)2 * k * ORA_NODE);
+  uint8_t* cr = (uint8_t*)malloc((size_t)2 * k * ORA_NODE);
+  uint8_t dah[32];
+  do {
+    int rc = ora_extend_commit(t->count, t->L, t->ods, eds, rr, cr, dah, 1);
+    if (rc != ORA_OK || memcmp(dah, t->dah0, 32) != 0) atomic_store(&t->rc, rc != ORA_OK ? rc : ORA_E_ARG);
+    atomic_fetch_add(&t->done, 1);
+  } while (now_s() < t->deadline);
+  free(eds);
+  free(rr);
+  free(cr);
+  return NULL;
+}
+
+long ora_extend_commit_throughput(int count, size_t share_len, const uint8_t* shares, int nthreads, double seconds,
+                                  double* elapsed) {
+  if (nthreads < 1) nthreads = 1;
+  tput_t t;
+  t.count = count;
+  t.L = share_len;
+  t.ods = shares;
+  atomic_init(&t.done, 0);
+  atomic_init(&t.rc, ORA_OK);
+  { /* expected DAH (every call must reproduce it) */
+    const int k = (int)lround(sqrt((double)count));
+    uint8_t* rr = (uint8_t*)malloc((size_t)2 * k * ORA_NODE);
+    uint8_t* cr = (uint8_t*)malloc((size_t)2 * k * ORA_NODE);
+    int rc = ora_extend_commit(count, share_len, shares, NULL, rr, cr, t.dah0, 1);
+    free(rr);
+    free(cr);
+    if (rc != ORA_OK) return rc;
+  }
+  const double t0 = now_s();
+  t.deadline = t0 + seconds;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, tput_worker, &t);
+  for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+  free(th);
+  if (elapsed) *elapsed = now_s() - t0;
+  if (atomic_load(&t.rc) != ORA_OK) return atomic_load(&t.rc);
+  return atomic_load(&t.done);
 }
 
 /* ------------------------------------------------------------------ */

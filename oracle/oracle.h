@@ -93,6 +93,11 @@ int ora_roots(int k, size_t share_len, const uint8_t* eds, uint8_t* row_roots, u
 /* DAH hash = RFC-6962 over row roots ‖ col roots (n roots per axis). */
 void ora_dah_hash(int n, const uint8_t* row_roots, const uint8_t* col_roots, uint8_t out[32]);
 /* da.ExtendShares + NewDataAvailabilityHeader on `count` shares. */
+/* Throughput sample (bench cpu_baseline): nthreads workers each run whole single-threaded
+ * ora_extend_commit calls on `shares` until `seconds` pass; returns blocks completed
+ * (negative ORA_E_* if any call failed or its DAH differed). */
+long ora_extend_commit_throughput(int count, size_t share_len, const uint8_t* shares, int nthreads, double seconds,
+                                  double* elapsed);
 int ora_extend_commit(int count, size_t share_len, const uint8_t* shares, uint8_t* eds_or_null,
                       uint8_t* row_roots, uint8_t* col_roots, uint8_t dah[32], int nthreads);
 

@@ -46,6 +46,9 @@ def lib():
         L.ora_roots.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, ctypes.c_int, P, P]
         L.ora_dah_hash.argtypes = [ctypes.c_int, P, P, P]
         L.ora_extend_commit.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, ctypes.c_int]
+        L.ora_extend_commit_throughput.argtypes = [ctypes.c_int, ctypes.c_size_t, P, ctypes.c_int, ctypes.c_double,
+                                                   ctypes.POINTER(ctypes.c_double)]
+        L.ora_extend_commit_throughput.restype = ctypes.c_long
         L.ora_repair.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, P]
         L.ora_gen_ods.argtypes = [ctypes.c_int, ctypes.c_uint64, P]
         _bind_inclusion(L)
@@ -141,6 +144,18 @@ def extend_commit(shares: np.ndarray, want_eds: bool = True, nthreads: int = 8):
     rc = lib().ora_extend_commit(count, L, _p(shares), _p(eds) if eds is not None else None,
                                  _p(rr), _p(cr), _p(dah), nthreads)
     return rc, eds, rr, cr, dah.tobytes()
+
+
+def extend_commit_throughput(shares: np.ndarray, nthreads: int, seconds: float):
+    """Blocks/s of single-threaded ExtendShares+NewDataAvailabilityHeader calls run by `nthreads` workers
+    on independent copies of one block for `seconds`. Returns (blocks, elapsed_s)."""
+    shares = np.ascontiguousarray(shares, np.uint8)
+    count, L = shares.shape
+    el = ctypes.c_double(0.0)
+    n = lib().ora_extend_commit_throughput(count, L, _p(shares), nthreads, seconds, ctypes.byref(el))
+    if n < 0:
+        raise RuntimeError(f"oracle throughput sample failed: {n}")
+    return int(n), el.value
 
 
 def nmt_axis_root(square_size: int, axis_index: int, leaves):

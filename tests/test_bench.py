@@ -1,0 +1,49 @@
+"""bench.py plumbing on CPU: --gpus N spawns N ranks itself (no torchrun), the ranks form a process group and
+the max-over-ranks timing collective runs; the CPU baseline sampler counts independent blocks."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_two_ranks():
+    r = _run_bench("--gpus", "2", "--dry-run")
+    assert r["n_gpus"] == 2 and r["ranks_seen"] == 2 and r["max_rank"] == 1
+
+
+def test_bench_spawns_four_ranks():
+    r = _run_bench("--gpus", "4", "--dry-run")
+    assert r["n_gpus"] == 4 and r["ranks_seen"] == 4
+
+
+def test_cpu_throughput_sampler():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    ods = O.gen_ods(8, 0xC0FFEE)
+    n, el = O.extend_commit_throughput(ods, 2, 0.2)
+    assert n >= 2 and el > 0.0
+
+
+def test_bench_workload_helpers():
+    sys.path.insert(0, ROOT)
+    import bench
+    import oracle_lib as O
+    # bench's generator is the oracle's ora_gen_ods (same SplitMix64 stream, sorted)
+    assert np.array_equal(bench.gen_ods(8, 0xC0FFEE + 3), O.gen_ods(8, 0xC0FFEE + 3))
+    assert bench.block_bytes(128) == 41989152
+    assert bench.block_compressions_ref(128) == 1573374
