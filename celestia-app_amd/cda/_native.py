@@ -192,8 +192,18 @@ class Context:
     def extend_commit_batch(self, ods, want_eds=True, eds_out=None):
         """ods: (nblocks, k*k, 512); eds_out: optional preallocated (nblocks, 4k^2, 512) uint8 output."""
         ods = np.ascontiguousarray(ods, np.uint8)
+        if ods.ndim != 3:
+            raise CdaError(E_ARG, "ods must be (nblocks, k*k, 512)")
         nb, kk, L = ods.shape
         k = int(round(kk ** 0.5))
+        if k * k != kk or L != SHARE_SIZE or nb == 0:
+            raise CdaError(E_ARG, "ods must be (nblocks, k*k, 512) with nblocks > 0")
+        if eds_out is not None:
+            # the library writes nblocks * 4k^2 * 512 bytes through this pointer: it must be exactly that array
+            if (not isinstance(eds_out, np.ndarray) or eds_out.dtype != np.uint8 or not eds_out.flags.c_contiguous
+                    or not eds_out.flags.writeable or eds_out.shape != (nb, 4 * k * k, L)):
+                raise CdaError(E_ARG, f"eds_out must be a writeable C-contiguous uint8 array of shape "
+                                      f"{(nb, 4 * k * k, L)}")
         eds = eds_out if eds_out is not None else (np.empty((nb, 4 * k * k, L), np.uint8) if want_eds else None)
         rr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
         cr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
@@ -269,14 +279,22 @@ class Context:
         return root.tobytes()
 
     def repair(self, eds, present, row_roots, col_roots):
+        rc, eds, pres, err = self.repair_status(eds, present, row_roots, col_roots)
+        _check(rc, err, self)
+        return eds, pres
+
+    def repair_status(self, eds, present, row_roots, col_roots):
+        """cda_repair without raising: (rc, eds, present, err) where eds/present hold the square as far as
+        it was repaired (rsmt2d leaves the square 'most repaired prior to the Byzantine axis')."""
         eds = np.ascontiguousarray(eds, np.uint8).copy()
         pres = np.ascontiguousarray(present, np.uint8).copy()
         w = len(row_roots)
+        if eds.shape[0] != w * w or eds.size != w * w * SHARE_SIZE or pres.size != w * w:
+            raise CdaError(E_ARG, "eds must be (2k)^2 x 512 bytes and present (2k)^2 flags")
         err = ErrInfo()
         rc = lib().cda_repair(self._h, w // 2, _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots, np.uint8)),
                               _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err))
-        _check(rc, err, self)
-        return eds, pres
+        return rc, eds, pres, err
 
     # ---- blob share commitments, node export, proofs ----
     def blob_commitments(self, namespaces, datas, share_versions=None, subtree_root_threshold=64):

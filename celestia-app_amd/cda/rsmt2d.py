@@ -141,14 +141,39 @@ class ExtendedDataSquare:
 
 
 def compute_extended_data_square(data, codec=None, tree_constructor=None):
-    """rsmt2d.ComputeExtendedDataSquare(data, codec, treeCreatorFn)."""
+    """rsmt2d.ComputeExtendedDataSquare(data, codec, treeCreatorFn).
+
+    The extension always runs on the device.  With no tree constructor, or wrapper.NewConstructor(k) (the one
+    pkg/da passes, data_availability_header.go:74), the fused device path also computes every root.  Any other
+    TreeConstructorFn (e.g. pkg/inclusion's EDSSubTreeRootCacher, nmt_caching.go:96-109) gets the reference's
+    semantics: rsmt2d builds one tree per axis through it, pushes that axis's cells in order and takes Root()."""
     codec = codec or LeoRSCodec()
     if len(data) > codec.max_chunks():
         raise ValueError("number of chunks exceeds the maximum")
     arr = np.stack([np.frombuffer(bytes(d), np.uint8) for d in data]) if len(data) else np.zeros((0, 512), np.uint8)
-    eds, rr, cr, _ = codec.ctx.extend_commit(arr)
     k = int(round(len(data) ** 0.5))
-    return ExtendedDataSquare(eds, 2 * k, k, codec, rr, cr)
+    fused = tree_constructor is None or getattr(tree_constructor, "cda_erasured_square_size", None) == k
+    eds, rr, cr, _ = codec.ctx.extend_commit(arr)
+    sq = ExtendedDataSquare(eds, 2 * k, k, codec, rr, cr)
+    if not fused:
+        sq._row_roots, sq._col_roots = _roots_through(sq, tree_constructor)
+    return sq
+
+
+
+
+def _roots_through(sq, tree_constructor):
+    """rsmt2d computeRoots with a caller's TreeConstructorFn: rows then columns, each axis pushed in order."""
+    roots = []
+    for axis, cells in ((ROW, sq.row), (COL, sq.col)):
+        out = []
+        for i in range(sq._width):
+            tree = tree_constructor(axis, i)
+            for share in cells(i):
+                tree.push(share)
+            out.append(np.frombuffer(bytes(tree.root()), np.uint8))
+        roots.append(np.stack(out))
+    return roots[0], roots[1]
 
 
 def import_extended_data_square(cells, codec=None):

@@ -56,4 +56,6 @@ def new_constructor(square_size, ctx=None):
     def new_tree(axis, axis_index):
         return ErasuredNamespacedMerkleTree(square_size, axis_index, ctx)
 
+    # marks the constructor whose trees the fused device path (cda_extend_commit) computes itself
+    new_tree.cda_erasured_square_size = int(square_size)
     return new_tree

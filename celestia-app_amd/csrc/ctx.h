@@ -25,6 +25,12 @@ struct cda_ctx {
   // CDA_CHUNK: blocks per sequential chunk on one stream (0 = whole batch at once)
   int chunk_blocks = 0;
   hipStream_t sub[kMaxSub] = {};
+  // Workspace ordering across streams: the device-resident entry points enqueue on the caller's
+  // stream but use this ctx's workspace (leaf/scratch records).  ws_event marks the end of the
+  // last such enqueue; synchronous entry points make `stream` wait on it, and device entry points
+  // wait on it and on `stream` (sync_ev), so no two uses of the workspace overlap.
+  hipEvent_t ws_event = nullptr, sync_ev = nullptr;
+  bool ws_pending = false;
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::string last_err;
   // workspace
@@ -63,10 +69,36 @@ int map_status(uint64_t st, int block, cda_err_info* err);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 
+// Synchronous entry points (work on c->stream): ordered after any device-resident enqueue.
 struct Lock {
   cda_ctx* c;
   std::lock_guard<std::recursive_mutex> g;
-  explicit Lock(cda_ctx* x) : c(x), g(x->mu) { (void)hipSetDevice(x->device); }
+  explicit Lock(cda_ctx* x) : c(x), g(x->mu) {
+    (void)hipSetDevice(x->device);
+    if (x->ws_pending) {
+      (void)hipStreamWaitEvent(x->stream, x->ws_event, 0);
+      x->ws_pending = false;
+    }
+  }
+};
+
+// Device-resident entry points enqueueing on the caller's stream `s`: ordered after the previous
+// users of the workspace (device enqueues on other streams, synchronous calls on c->stream), and
+// marking their own end for the next user.
+struct DevLock {
+  cda_ctx* c;
+  hipStream_t s;
+  std::lock_guard<std::recursive_mutex> g;
+  DevLock(cda_ctx* x, hipStream_t st) : c(x), s(st), g(x->mu) {
+    (void)hipSetDevice(x->device);
+    (void)hipEventRecord(x->sync_ev, x->stream);
+    (void)hipStreamWaitEvent(s, x->sync_ev, 0);
+    if (x->ws_pending) (void)hipStreamWaitEvent(s, x->ws_event, 0);
+  }
+  ~DevLock() {
+    (void)hipEventRecord(c->ws_event, s);
+    c->ws_pending = true;
+  }
 };
 
 }  // namespace cda

@@ -318,7 +318,9 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
   if (const char* e = getenv("CDA_PIPELINE")) c->pipe_chunks = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("CDA_CHUNK")) c->chunk_blocks = std::max(0, atoi(e));
-  bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
+  bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
     ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
@@ -345,6 +347,8 @@ void cda_free(cda_ctx* c) {
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->ws_event) (void)hipEventDestroy(c->ws_event);
+    if (c->sync_ev) (void)hipEventDestroy(c->sync_ev);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -449,8 +453,8 @@ int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const voi
   if (!c || !d_ods || !d_eds || !d_roots || !d_dah || !d_status || nblocks == 0) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
   if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
-  Lock l(c);
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  DevLock l(c, s);
   return enqueue_pipeline(c, k, nblocks, (const uint8_t*)d_ods, (uint8_t*)d_eds, d_roots, d_dah,
                           (unsigned long long*)d_status, s);
 }
@@ -460,8 +464,8 @@ int cda_rs_encode_device(cda_ctx* c, uint32_t k, uint32_t shard_len, uint32_t nc
   if (!c || !d_src || !d_dst || k == 0 || k > 32768) return CDA_E_ARG;
   if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
   if (ncw == 0) return CDA_OK;
-  Lock l(c);
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  DevLock l(c, s);
   RsJob j{};
   j.src = (const uint8_t*)d_src;
   j.src_cw = src_cw;
@@ -488,8 +492,8 @@ int cda_nmt_roots_device(cda_ctx* c, uint32_t k, const void* d_eds, uint32_t axi
   if (k > kMaxDeviceK || first_index + naxes > w || !is_pow2(nleaves) || leaf_off % nleaves || leaf_off + nleaves > w)
     return CDA_E_ARG;
   if (naxes == 0) return CDA_OK;
-  Lock l(c);
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  DevLock l(c, s);
   const size_t recs = (size_t)naxes * nleaves * CDA_REC_BYTES;
   int rc;
   if ((rc = ensure(c, c->leaf, recs)) || (rc = ensure(c, c->scratch, recs))) return rc;
@@ -505,8 +509,8 @@ int cda_nmt_roots_device(cda_ctx* c, uint32_t k, const void* d_eds, uint32_t axi
 int cda_nmt_fold_device(cda_ctx* c, uint32_t ntrees, uint32_t n, const void* d_nodes, void* d_roots, void* stream) {
   if (!c || !d_nodes || !d_roots || !is_pow2(n)) return CDA_E_ARG;
   if (ntrees == 0) return CDA_OK;
-  Lock l(c);
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  DevLock l(c, s);
   const size_t bytes = (size_t)ntrees * n * CDA_REC_BYTES;
   if (n == 1) return dev_ok(c, hipMemcpyAsync(d_roots, d_nodes, bytes, hipMemcpyDeviceToDevice, s), "D2D") ? CDA_OK
                                                                                                           : CDA_E_DEVICE;
@@ -519,8 +523,8 @@ int cda_nmt_fold_device(cda_ctx* c, uint32_t ntrees, uint32_t n, const void* d_n
 
 int cda_dah_device(cda_ctx* c, uint32_t n_total, const void* d_roots, void* d_dah, void* stream) {
   if (!c || !d_roots || !d_dah || n_total == 0) return CDA_E_ARG;
-  Lock l(c);
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+  DevLock l(c, s);
   ProfScope ps(c, "dah", s);
   const int lr = launch_dah(d_roots, d_dah, (int)n_total, 1, s);
   if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
@@ -585,6 +589,7 @@ int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_root
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !eds || !row_roots || !col_roots || !dah) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   Lock l(c);
   const uint32_t w = 2 * k;
   const size_t eds_b = (size_t)w * w * CDA_SHARE, roots_b = (size_t)2 * w * CDA_REC_BYTES;
@@ -612,7 +617,8 @@ int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_root
   }
   {
     ProfScope ps(c, "dah", s);
-    if (launch_dah(c->roots.p, c->dah.p, (int)(2 * w), 1, s)) return CDA_E_DEVICE;
+    const int lr = launch_dah(c->roots.p, c->dah.p, (int)(2 * w), 1, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   std::vector<uint8_t> recs(roots_b);
   uint64_t st = 0;
@@ -666,12 +672,18 @@ int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uin
                       const uint8_t* leaves, uint8_t* root, cda_err_info* err) {
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !root || (n && !leaves) || square_size == 0) return CDA_E_ARG;
-  // ErasuredNamespacedMerkleTree.Push checks, in the reference's order (nmt_wrapper.go:94-99)
-  for (uint32_t i = 0; i < n; i++) {
-    if (axis_index + 1 > 2 * square_size || (uint64_t)i + 1 > 2 * square_size)
-      return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, (int)i, -1), CDA_E_PUSH_PAST;
-    if (leaf_len < CDA_NAMESPACE_SIZE) return set_err(err, CDA_E_NS_SHORT, -1, (int)axis_index, (int)i, -1), CDA_E_NS_SHORT;
-  }
+  // ErasuredNamespacedMerkleTree.Push checks (nmt_wrapper.go:94-99) happen leaf by leaf in the
+  // reference, before nmt's order check of the same leaf: the bounds check fails first at leaf 0
+  // (axis index out of range) or at leaf 2k (pushed past the square), the namespace-length check at
+  // leaf 0.  An order violation at a leaf j < 2k therefore wins over a push past the square; the
+  // device pass below only looks at the leaves the reference would have accepted.
+  if (n > 0 && axis_index + 1 > 2 * square_size)
+    return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, 0, -1), CDA_E_PUSH_PAST;
+  if (n > 0 && leaf_len < CDA_NAMESPACE_SIZE)
+    return set_err(err, CDA_E_NS_SHORT, -1, (int)axis_index, 0, -1), CDA_E_NS_SHORT;
+  const uint64_t push_limit = 2 * square_size;
+  const bool past = (uint64_t)n > push_limit;
+  if (past) n = (uint32_t)push_limit;
   if (n == 0) {  // EmptyRoot: 0x00*58 ‖ SHA256("")
     static const uint8_t kEmpty[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
                                        0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
@@ -712,6 +724,7 @@ int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uin
     return CDA_E_DEVICE;
   flush_profile(c);
   if (st != ~0ull) return set_err(err, CDA_E_NS_ORDER, -1, (int)axis_index, (int)st, -1), CDA_E_NS_ORDER;
+  if (past) return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, (int)push_limit, -1), CDA_E_PUSH_PAST;
   memcpy(root, rec, CDA_NODE_SIZE);
   return CDA_OK;
 }
@@ -725,10 +738,10 @@ int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uin
 //     without progress is ErrUnrepairableDataSquare.
 // The host replays exactly that order on the presence bitmap (control only) and
 // runs every decode / root / re-encode on the GPU, batching consecutive
-// operations that are already decodable at the batch start.  On a Byzantine
-// failure the cells of the failing operation and of later operations in its
-// batch are marked missing again, leaving the square "most repaired prior to the
-// Byzantine axis" as the reference does.
+// operations that are already decodable at the batch start; a batch with a
+// failing root check is replayed one operation at a time (see below), so a
+// Byzantine report and the square left "most repaired prior to the Byzantine
+// axis" are exactly the sequential reference's.
 namespace {
 inline int enc_axis(int axis, int idx) { return (axis << 24) | idx; }
 }
@@ -902,12 +915,16 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
         progress = true;
       }
     }
-    // execute in batches of operations already decodable at the batch start
-    size_t b0 = 0;
-    while (b0 < ops.size()) {
-      size_t b1 = b0;
-      while (b1 < ops.size() && b1 - b0 < trees_cap / 2 && count(P, ops[b1].axis, ops[b1].idx, -1) >= K) b1++;
-      if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
+    // Execute in batches of operations already decodable at the batch start.  A batch whose every
+    // root check passes equals the sequential rsmt2d run: each checked axis then holds its committed
+    // values, so every decode saw only true shares and the sequential decode (with more shares) gives
+    // the same bytes.  A batch with any failing check is replayed one operation at a time with the
+    // presence that operation sees in rsmt2d's order, so Byzantine reports (axis, index, the square
+    // repaired so far) are exactly the sequential ones even when a row and a column of the batch
+    // write the same cell.
+    // run_ops: decode ops [b0, b1) with the presence P, verify own + orthogonal roots in order.
+    // Returns CDA_OK, CDA_E_BYZANTINE (*bad = failing axis code) or an error; P is not modified.
+    auto run_ops = [&](size_t b0, size_t b1, int* bad) -> int {
       const int nb = (int)(b1 - b0);
       std::vector<long long> off(nb), stride(nb);
       std::vector<uint8_t> pres((size_t)nb * w);
@@ -932,28 +949,39 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
         vaxes.push_back(enc_axis(ops[q].axis, ops[q].idx));
         for (int o : ops[q].ortho) vaxes.push_back(o);
       }
-      size_t t = 0;
       for (size_t v0 = 0; v0 < vaxes.size(); v0 += trees_cap) {  // chunks of at most trees_cap trees
         std::vector<int> chunk(vaxes.begin() + v0, vaxes.begin() + std::min(vaxes.size(), v0 + trees_cap));
-        if ((rc = roots_of(chunk))) return rc;
-        for (size_t u = 0; u < chunk.size(); u++, t++) {
-          if (root_ok(u, chunk[u])) continue;
-          // locate the operation owning verification t; earlier operations stay applied
-          size_t acc = 0;
-          for (size_t q = b0; q < b1; q++) {
-            const size_t nv = 1 + ops[q].ortho.size();
-            if (t < acc + nv) {
-              for (size_t e = b0; e < q; e++)
-                for (int j = 0; j < w; j++) P[cell(ops[e].axis, ops[e].idx, j)] = 1;
-              const int bad = t == acc ? enc_axis(ops[q].axis, ops[q].idx) : ops[q].ortho[t - acc - 1];
-              return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
-            }
-            acc += nv;
+        if (int r2 = roots_of(chunk)) return r2;
+        for (size_t u = 0; u < chunk.size(); u++)
+          if (!root_ok(u, chunk[u])) {
+            *bad = chunk[u];
+            return CDA_E_BYZANTINE;
           }
-        }
       }
-      for (size_t q = b0; q < b1; q++)
-        for (int j = 0; j < w; j++) P[cell(ops[q].axis, ops[q].idx, j)] = 1;
+      return CDA_OK;
+    };
+    auto apply = [&](size_t q) {
+      for (int j = 0; j < w; j++) P[cell(ops[q].axis, ops[q].idx, j)] = 1;
+    };
+    size_t b0 = 0;
+    while (b0 < ops.size()) {
+      size_t b1 = b0;
+      while (b1 < ops.size() && b1 - b0 < trees_cap / 2 && count(P, ops[b1].axis, ops[b1].idx, -1) >= K) b1++;
+      if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
+      int bad = 0;
+      rc = run_ops(b0, b1, &bad);
+      if (rc == CDA_E_BYZANTINE && b1 - b0 > 1) {
+        for (size_t q = b0; q < b1; q++) {  // sequential replay of the failed batch
+          rc = run_ops(q, q + 1, &bad);
+          if (rc == CDA_E_BYZANTINE) return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
+          if (rc) return rc;
+          apply(q);
+        }
+      } else {
+        if (rc == CDA_E_BYZANTINE) return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
+        if (rc) return rc;
+        for (size_t q = b0; q < b1; q++) apply(q);
+      }
       b0 = b1;
     }
     if (solved) break;

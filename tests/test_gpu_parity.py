@@ -373,3 +373,121 @@ def test_concurrent_calls_on_one_context(ctx):
     for t in threads:
         t.join(120)
     assert not errors, errors
+
+
+# ---- Repair under Byzantine input: batched GPU execution must equal rsmt2d's sequential order ------------
+def _check_repair_exact(ctx, bad, pres, rr, cr):
+    """rc, (axis, index), the presence map and every present cell of the partially repaired square equal the
+    oracle's sequential rsmt2d restatement (oracle/da.c ora_repair)."""
+    rc_o, eds_o, p_o, ax_o, ix_o = O.repair(bad, pres, rr, cr)
+    rc_g, eds_g, p_g, err = ctx.repair_status(bad, pres, rr, cr)
+    assert rc_g == rc_o, (rc_g, rc_o)
+    if rc_o == O.E_BYZANTINE:
+        assert (err.axis, err.index) == (ax_o, ix_o)
+    assert np.array_equal(p_g, p_o)
+    m = p_o.astype(bool)
+    assert np.array_equal(eds_g[m], eds_o[m])
+    return rc_o, (ax_o, ix_o)
+
+
+def test_repair_byzantine_row_and_column_share_a_missing_cell(ctx):
+    """row 0 (honest) and column 5 (one corrupted present cell) are both decodable in the first sweep
+    and share the missing cell (0, 5).  rsmt2d repairs row 0 first and then reports column 5."""
+    k = 8
+    w = 2 * k
+    eds, rr, cr = _square(k, 31)
+    rng = np.random.default_rng(8)
+    pres = (rng.random((w, w)) < 0.75).astype(np.uint8)
+    pres[0, 5] = 0          # shared missing cell of row 0 and column 5
+    pres[10, 5] = 1         # corrupted present cell, in a row processed after column 5
+    pres[10, 11] = 0        # row 10 incomplete, so the sanity check does not see it
+    pres[3, 5] = 0          # column 5 incomplete
+    bad = eds.copy()
+    bad[10 * w + 5, 100] ^= 0x5A
+    rc, (ax, ix) = _check_repair_exact(ctx, bad, pres.reshape(-1), rr, cr)
+    assert rc == O.E_BYZANTINE and (ax, ix) == (1, 5)
+
+
+@pytest.mark.parametrize("k,frac,nbad,seed", [(8, 0.6, 1, 1), (8, 0.7, 2, 2), (16, 0.6, 1, 3), (32, 0.55, 2, 4),
+                                              (32, 0.7, 3, 5), (128, 0.55, 1, 6), (128, 0.65, 2, 7),
+                                              (128, 0.6, 1, 8)])
+def test_repair_byzantine_random_matches_sequential(ctx, k, frac, nbad, seed):
+    """Random erasures plus corrupted present cells: the GPU's batched crossword reports the same error, axis and
+    index as the sequential oracle and leaves the same partially repaired square."""
+    w = 2 * k
+    eds, rr, cr = _square(k, 500 + seed)
+    rng = np.random.default_rng(seed)
+    pres = (rng.random(w * w) < frac).astype(np.uint8)
+    bad = eds.copy()
+    for idx in rng.choice(np.flatnonzero(pres), nbad, replace=False):
+        bad[idx, rng.integers(0, 512)] ^= 1 + rng.integers(0, 255)
+    _check_repair_exact(ctx, bad, pres, rr, cr)
+
+
+def test_compute_eds_honours_custom_tree_constructor(ctx):
+    """A TreeConstructorFn other than wrapper.NewConstructor is called the rsmt2d way:
+    one tree per axis, the axis's cells pushed in order; the roots are the custom trees' roots."""
+    from cda import rsmt2d, wrapper
+    k = 4
+    ods = O.gen_ods(k, 5)
+    calls = []
+
+    class CountingTree(wrapper.ErasuredNamespacedMerkleTree):
+        def push(self, data):
+            calls.append((self.axis_index, self.share_index))
+            super().push(data)
+
+    def ctor(axis, index):
+        return CountingTree(k, index, ctx)
+
+    codec = rsmt2d.LeoRSCodec(ctx)
+    sq = rsmt2d.compute_extended_data_square([bytes(r) for r in ods], codec, ctor)
+    assert len(calls) == 2 * (2 * k) * (2 * k)
+    ref = rsmt2d.compute_extended_data_square([bytes(r) for r in ods], codec, wrapper.new_constructor(k, ctx))
+    assert sq.row_roots() == ref.row_roots() and sq.col_roots() == ref.col_roots()
+
+
+def test_device_and_sync_calls_share_the_workspace(ctx):
+    """cda_extend_commit_device enqueues on the caller's stream and uses the ctx workspace; a
+    synchronous call issued right after must not overwrite it before the device call's kernels ran."""
+    import torch
+    k, B = 32, 8
+    w = 2 * k
+    ods = np.stack([O.gen_ods(k, 900 + b) for b in range(B)])
+    dev = torch.device("cuda", 0)
+    d_ods = torch.from_numpy(ods).to(dev)
+    d_eds = torch.empty((B, w * w, 512), dtype=torch.uint8, device=dev)
+    d_roots = torch.empty((B, 2 * w, 96), dtype=torch.uint8, device=dev)
+    d_dah = torch.empty((B, 32), dtype=torch.uint8, device=dev)
+    d_status = torch.empty((B,), dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    other = O.gen_ods(64, 77)
+    _, _, _, dah_other = O.extend_commit(other)
+    for _ in range(3):
+        ctx.extend_commit_device(k, B, d_ods.data_ptr(), d_eds.data_ptr(), d_roots.data_ptr(), d_dah.data_ptr(),
+                                 d_status.data_ptr(), s.cuda_stream)
+        assert ctx.extend_commit(other)[3] == dah_other  # synchronous, on the ctx's own stream
+    s.synchronize()
+    for b in range(B):
+        assert d_dah[b].cpu().numpy().tobytes() == O.extend_commit(ods[b])[4]
+
+
+def test_axis_root_order_error_wins_over_push_past(ctx):
+    """the reference Push validates leaf by leaf, so an order violation at leaf 3 is reported even when
+    the caller pushes more than 2k leaves; a sorted over-long push reports PUSH_PAST at leaf 2k."""
+    from cda import CdaError
+    k = 4
+    ods = O.gen_ods(8, 41)
+    leaves = sorted(bytes(r) for r in ods[:k])
+    bad = leaves[:3] + [leaves[0]] + [bytes(ods[i]) for i in range(k, 2 * k + 3)]  # order broken at leaf 3
+    rc_o, _, leaf_o = O.nmt_axis_root(k, 0, bad)
+    assert rc_o == O.E_NS_ORDER and leaf_o == 3
+    with pytest.raises(CdaError) as ei:
+        ctx.nmt_axis_root(k, 0, bad)
+    assert ei.value.code == O.E_NS_ORDER and ei.value.leaf == 3
+    good = leaves + [bytes(ods[i]) for i in range(k, 2 * k + 2)]
+    rc_o, _, leaf_o = O.nmt_axis_root(k, 0, good)
+    assert rc_o == O.E_PUSH_PAST and leaf_o == 2 * k
+    with pytest.raises(CdaError) as ei:
+        ctx.nmt_axis_root(k, 0, good)
+    assert ei.value.code == O.E_PUSH_PAST and ei.value.leaf == 2 * k
