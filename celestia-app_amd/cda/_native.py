@@ -46,6 +46,8 @@ EXPORTS = [
     "cda_rs_encode_device", "cda_nmt_roots_device", "cda_nmt_fold_device", "cda_dah_device",
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
     "cda_blob_commitments", "cda_merkle_roots", "cda_extend_commit_nodes", "cda_share_inclusion_proof",
+    "cda_host_alloc", "cda_host_free", "cda_multi_init", "cda_multi_free", "cda_multi_device_count",
+    "cda_multi_context", "cda_multi_extend_commit_batch",
 ]
 
 
@@ -110,6 +112,13 @@ def lib():
                 "cda_extend_commit_nodes": (I32, [P, U32, U32, P, P, P, P, P, P, P, P, P]),
                 "cda_share_inclusion_proof": (I32, [P, U32, U32, P, U32, U32, P, P, P, P, P, P, P, P, P,
                                                       P]),
+                "cda_host_alloc": (I32, [P, SZ, ctypes.POINTER(P)]),
+                "cda_host_free": (I32, [P, P]),
+                "cda_multi_init": (I32, [U32, ctypes.POINTER(P)]),
+                "cda_multi_free": (None, [P]),
+                "cda_multi_device_count": (I32, [P]),
+                "cda_multi_context": (P, [P, I32]),
+                "cda_multi_extend_commit_batch": (I32, [P, U32, U32, P, P, P, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)
@@ -139,6 +148,10 @@ def _check(rc, err=None, ctx=None):
 
 class Context:
     """One cda_ctx bound to one HIP device (one process per GPU)."""
+
+    def pinned(self, shape, dtype=np.uint8):
+        """Pinned host buffer (cda_host_alloc) for the host-buffer batch path."""
+        return PinnedBuffer(self, shape, dtype)
 
     def __init__(self, device=0):
         h = ctypes.c_void_p()
@@ -191,23 +204,8 @@ class Context:
 
     def extend_commit_batch(self, ods, want_eds=True, eds_out=None):
         """ods: (nblocks, k*k, 512); eds_out: optional preallocated (nblocks, 4k^2, 512) uint8 output."""
-        ods = np.ascontiguousarray(ods, np.uint8)
-        if ods.ndim != 3:
-            raise CdaError(E_ARG, "ods must be (nblocks, k*k, 512)")
-        nb, kk, L = ods.shape
-        k = int(round(kk ** 0.5))
-        if k * k != kk or L != SHARE_SIZE or nb == 0:
-            raise CdaError(E_ARG, "ods must be (nblocks, k*k, 512) with nblocks > 0")
-        if eds_out is not None:
-            # the library writes nblocks * 4k^2 * 512 bytes through this pointer: it must be exactly that array
-            if (not isinstance(eds_out, np.ndarray) or eds_out.dtype != np.uint8 or not eds_out.flags.c_contiguous
-                    or not eds_out.flags.writeable or eds_out.shape != (nb, 4 * k * k, L)):
-                raise CdaError(E_ARG, f"eds_out must be a writeable C-contiguous uint8 array of shape "
-                                      f"{(nb, 4 * k * k, L)}")
-        eds = eds_out if eds_out is not None else (np.empty((nb, 4 * k * k, L), np.uint8) if want_eds else None)
-        rr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
-        cr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
-        dah = np.empty((nb, 32), np.uint8)
+        ods, k, eds, rr, cr, dah = _batch_outputs(ods, want_eds, eds_out)
+        nb = len(ods)
         err = ErrInfo()
         rc = lib().cda_extend_commit_batch(self._h, k, nb, _p(ods), _p(eds), _p(rr), _p(cr), _p(dah),
                                            ctypes.byref(err))
@@ -394,6 +392,84 @@ class Context:
 
 _default = None
 _default_lock = threading.Lock()
+
+
+def _batch_outputs(ods, want_eds, eds_out):
+    """Shape checks shared by the batch entry points; returns (ods, k, eds, rr, cr, dah)."""
+    ods = np.ascontiguousarray(ods, np.uint8)
+    if ods.ndim != 3:
+        raise CdaError(E_ARG, "ods must be (nblocks, k*k, 512)")
+    nb, kk, L = ods.shape
+    k = int(round(kk ** 0.5))
+    if k * k != kk or L != SHARE_SIZE or nb == 0:
+        raise CdaError(E_ARG, "ods must be (nblocks, k*k, 512) with nblocks > 0")
+    if eds_out is not None:
+        # the library writes nblocks * 4k^2 * 512 bytes through this pointer: it must be exactly that array
+        if (not isinstance(eds_out, np.ndarray) or eds_out.dtype != np.uint8 or not eds_out.flags.c_contiguous
+                or not eds_out.flags.writeable or eds_out.shape != (nb, 4 * k * k, L)):
+            raise CdaError(E_ARG, f"eds_out must be a writeable C-contiguous uint8 array of shape {(nb, 4 * k * k, L)}")
+    eds = eds_out if eds_out is not None else (np.empty((nb, 4 * k * k, L), np.uint8) if want_eds else None)
+    rr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
+    cr = np.empty((nb, 2 * k, NODE_SIZE), np.uint8)
+    dah = np.empty((nb, 32), np.uint8)
+    return ods, k, eds, rr, cr, dah
+
+
+class PinnedBuffer:
+    """Pinned host memory from cda_host_alloc, viewed as a numpy array (freed with the object)."""
+
+    def __init__(self, ctx, shape, dtype=np.uint8):
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        ptr = ctypes.c_void_p()
+        _check(lib().cda_host_alloc(ctx._h, nbytes, ctypes.byref(ptr)), ctx=ctx)
+        self._ctx, self._ptr = ctx, ptr
+        buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(ptr.value)
+        self.array = np.frombuffer(buf, np.uint8, count=nbytes).view(dtype).reshape(shape)
+
+    def free(self):
+        if self._ptr is not None and self._ctx._h:
+            lib().cda_host_free(self._ctx._h, self._ptr)
+        self._ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class MultiContext:
+    """cda_multi: one handle over several GPUs of this process (device mask; 0 = all visible)."""
+
+    def __init__(self, device_mask=0):
+        h = ctypes.c_void_p()
+        rc = lib().cda_multi_init(device_mask, ctypes.byref(h))
+        if rc != OK:
+            raise CdaError(rc, "cda_multi_init failed")
+        self._h = h
+
+    @property
+    def device_count(self):
+        return lib().cda_multi_device_count(self._h)
+
+    def extend_commit_batch(self, ods, want_eds=True, eds_out=None):
+        ods, k, eds, rr, cr, dah = _batch_outputs(ods, want_eds, eds_out)
+        err = ErrInfo()
+        rc = lib().cda_multi_extend_commit_batch(self._h, k, len(ods), _p(ods), _p(eds), _p(rr), _p(cr), _p(dah),
+                                                 ctypes.byref(err))
+        _check(rc, err)
+        return eds, rr, cr, dah
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().cda_multi_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def default_context():

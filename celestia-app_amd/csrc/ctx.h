@@ -31,6 +31,10 @@ struct cda_ctx {
   // wait on it and on `stream` (sync_ev), so no two uses of the workspace overlap.
   hipEvent_t ws_event = nullptr, sync_ev = nullptr;
   bool ws_pending = false;
+  // host-buffer batch pipeline (host_pipeline.cpp): copy streams and per-slot events
+  static constexpr int kSlots = 3;
+  hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;
+  hipEvent_t ev_h2d[kSlots] = {}, ev_comp[kSlots] = {}, ev_d2h[kSlots] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::string last_err;
   // workspace
@@ -66,6 +70,13 @@ void set_err(cda_err_info* e, int code, int axis, int index, int leaf, int block
 void pack_roots(const uint8_t* recs, uint32_t n, uint8_t* out);
 // device status word -> CDA_OK / CDA_E_NS_ORDER (+ err detail)
 int map_status(uint64_t st, int block, cda_err_info* err);
+// whole block pipeline of nblocks device-resident blocks on stream s (engine.cpp)
+int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
+                     void* d_dah, unsigned long long* d_status, hipStream_t s);
+// host-buffer batch as an H2D / compute / D2H pipeline (host_pipeline.cpp); caller holds the lock
+int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
+                    uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err, int block0);
+void free_pipeline(cda_ctx* c);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 

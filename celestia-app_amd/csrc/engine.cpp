@@ -346,6 +346,7 @@ void cda_free(cda_ctx* c) {
       if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
+    free_pipeline(c);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
     if (c->sync_ev) (void)hipEventDestroy(c->sync_ev);
@@ -538,6 +539,8 @@ int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
   if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   Lock l(c);
+  if (nblocks > 1 && !c->prof) return batch_pipelined(c, k, nblocks, ods, eds_or_null, row_roots, col_roots, dah, err, 0);
+  // one block (or profiling, where kernels must not overlap the event brackets): serial on c->stream
   const uint32_t w = 2 * k;
   const size_t ods_b = (size_t)nblocks * k * k * CDA_SHARE, eds_b = (size_t)nblocks * w * w * CDA_SHARE;
   const size_t roots_b = (size_t)nblocks * 2 * w * CDA_REC_BYTES;

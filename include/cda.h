@@ -10,7 +10,10 @@
  * Threading: a cda_ctx serialises its own calls with an internal mutex, so the
  * entry points are re-entrant from concurrent goroutines (rsmt2d calls
  * Codec.Encode / Decode / NewTree concurrently per axis); use one ctx per OS
- * thread for parallel submission.
+ * thread for parallel submission.  The device-resident entry points (..._device)
+ * enqueue on the caller's stream but share the ctx's workspace: the ctx orders
+ * them after its earlier work and every later call after them (events), so
+ * mixing them with the synchronous calls is safe.
  */
 #ifndef CDA_H
 #define CDA_H
@@ -100,6 +103,30 @@ int cda_extend_commit(cda_ctx* ctx, uint32_t count, uint32_t share_len, const ui
 int cda_extend_commit_batch(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const uint8_t* ods,
                             uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                             cda_err_info* err);
+
+/* Host buffers are streamed through the GPU in chunks: H2D of chunk i+1, the extension and trees
+ * of chunk i and D2H of chunk i-1 overlap on three streams (PCIe full duplex).  Pageable memory
+ * works; memory from cda_host_alloc (pinned) avoids the runtime's staging copies. */
+
+/* Pinned host memory for share / EDS buffers (hipHostMalloc); free with cda_host_free. */
+int cda_host_alloc(cda_ctx* ctx, size_t bytes, void** out);
+int cda_host_free(cda_ctx* ctx, void* p);
+
+/* ---- multi-device batch (SURVEY.md §8b "batch ... plus a device mask", §8e) ----
+ * One handle over the GPUs in `device_mask` (bit d = HIP device d; 0 = all visible devices), one
+ * cda_ctx per device.  cda_multi_extend_commit_batch shards the nblocks independent blocks into
+ * contiguous ranges, one per device, each streamed by its own host thread (no collective: blocks are
+ * independent).  Buffers and errors as cda_extend_commit_batch; err->block is the global block index
+ * of the lowest failing block. */
+typedef struct cda_multi cda_multi;
+int cda_multi_init(uint32_t device_mask, cda_multi** out);
+void cda_multi_free(cda_multi* m);
+int cda_multi_device_count(const cda_multi* m);
+/* The per-device context i (0-based, in device order) for the single-device entry points. */
+cda_ctx* cda_multi_context(cda_multi* m, int i);
+int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, const uint8_t* ods,
+                                  uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                                  cda_err_info* err);
 
 /* Device-resident form (pointers are device memory of this ctx's GPU; `stream`
  * is a hipStream_t or NULL for the null stream).  Asynchronous: returns after

@@ -39,6 +39,7 @@ for k, cs in counters.items():
     if k.startswith("__amd"):
         continue
     row = {c: sum(v) / len(v) for c, v in cs.items()}
+    row["bench_batch"] = int(os.environ.get("BENCH_BATCH", "128"))  # blocks per bench step when profiled
     if "FETCH_SIZE" in row and "WRITE_SIZE" in row:
         row["hbm_bytes_corrected"] = (2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024
     if k in durations:
@@ -49,12 +50,14 @@ json.dump(summary, open(os.path.join(dst, f"{tag}_counters.json"), "w"), indent=
 with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
     f.write(f"# rocprofv3 summary ({tag})\n\nSource: scripts/profile.sh (bench.py --steps 5 --warmup 1), "
             "kernel trace + separate PMC passes.\n\n")
-    f.write("| kernel | avg ns | dispatches | VALU instr/wave | issue-stall frac | waitcnt/barrier frac | FETCH KB | WRITE KB | eff. clock GHz |\n|---|---|---|---|---|---|---|---|---|\n")
+    f.write("| kernel | avg ns | dispatches | VALU instr/wave | issue-stall frac | waitcnt/barrier frac | FETCH KB | WRITE KB | eff. clock GHz | VALU busy (ACTIVE_INST_VALU) |\n|---|---|---|---|---|---|---|---|---|---|\n")
     for k, r in sorted(summary.items(), key=lambda kv: -kv[1].get("avg_duration_ns", 0) * kv[1].get("dispatches", 0)):
         vpw = r.get("SQ_INSTS_VALU", 0) / r["SQ_WAVES"] if r.get("SQ_WAVES") else 0
         stall = r.get("SQ_WAIT_INST_ANY", 0) / r["SQ_WAVE_CYCLES"] if r.get("SQ_WAVE_CYCLES") else 0
         wait = r.get("SQ_WAIT_ANY", 0) / r["SQ_WAVE_CYCLES"] if r.get("SQ_WAVE_CYCLES") else 0
         clk = r.get("GRBM_GUI_ACTIVE", 0) / 8 / r["avg_duration_ns"] if r.get("avg_duration_ns") else 0
+        # SQ_ACTIVE_INST_VALU: quad-cycles waves spend issuing VALU, summed over the chip's 1024 SIMDs
+        busy = r.get("SQ_ACTIVE_INST_VALU", 0) * 4 / (1024 * r["GRBM_GUI_ACTIVE"] / 8) if r.get("GRBM_GUI_ACTIVE") else 0
         f.write(f"| {k} | {r.get('avg_duration_ns', 0):.0f} | {r.get('dispatches', 0)} | {vpw:.0f} | {stall:.2f} | "
-                f"{wait:.2f} | {r.get('FETCH_SIZE', 0):.0f} | {r.get('WRITE_SIZE', 0):.0f} | {clk:.2f} |\n")
+                f"{wait:.2f} | {r.get('FETCH_SIZE', 0):.0f} | {r.get('WRITE_SIZE', 0):.0f} | {clk:.2f} | {busy:.2f} |\n")
 print(open(os.path.join(dst, f"{tag}_summary.md")).read())

@@ -105,6 +105,67 @@ def test_batch_k128_pipeline(streams, monkeypatch):
         c.close()
 
 
+@pytest.mark.parametrize("k,nb,want_eds", [(8, 2, True), (32, 5, True), (32, 33, False), (64, 9, True),
+                                           (128, 2, True), (128, 13, True), (128, 13, False)])
+def test_batch_host_pipeline(ctx, k, nb, want_eds):
+    """cda_extend_commit_batch streams host buffers in chunks over three streams (H2D / compute / D2H, 3 device
+    slots): every block's EDS, roots and DAH still equal the oracle's, for chunk counts below, at and above the
+    slot count and a ragged last chunk."""
+    ods = np.stack([O.gen_ods(k, 0xD00D + 7 * b + k) for b in range(nb)])
+    eds, rr, cr, dah = ctx.extend_commit_batch(ods, want_eds=want_eds)
+    for b in range(nb):
+        rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods[b])
+        if want_eds:
+            assert np.array_equal(eds[b], eds_o), f"block {b} EDS differs"
+        assert np.array_equal(rr[b], rr_o) and np.array_equal(cr[b], cr_o), f"block {b} roots differ"
+        assert dah[b].tobytes() == dah_o
+
+
+def test_batch_host_pipeline_pinned_buffers(ctx):
+    """The same path with pinned host buffers (cda_host_alloc), as a cgo caller can allocate them."""
+    k, nb = 64, 10
+    src = np.stack([O.gen_ods(k, 0xAB + b) for b in range(nb)])
+    pin_in = ctx.pinned(src.shape)
+    pin_out = ctx.pinned((nb, 4 * k * k, 512))
+    pin_in.array[:] = src
+    eds, rr, cr, dah = ctx.extend_commit_batch(pin_in.array, eds_out=pin_out.array)
+    for b in (0, nb // 2, nb - 1):
+        rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(src[b])
+        assert np.array_equal(eds[b], eds_o) and dah[b].tobytes() == dah_o
+    pin_in.free()
+    pin_out.free()
+
+
+def test_batch_eds_out_is_validated(ctx):
+    from cda import CdaError
+    ods = np.stack([O.gen_ods(8, b) for b in range(2)])
+    for bad in (np.empty((2, 256, 511), np.uint8), np.empty((2, 256, 512), np.int8),
+                np.empty((2, 256, 1024), np.uint8)[:, :, ::2]):
+        with pytest.raises(CdaError):
+            ctx.extend_commit_batch(ods, eds_out=bad)
+
+
+def test_multi_device_batch():
+    """cda_multi over every visible device (device mask 0): contiguous block ranges per device, no collective;
+    results equal the single-context batch.  On a one-GPU box this exercises the one-device path."""
+    import cda
+    m = cda.MultiContext(0)
+    try:
+        assert m.device_count >= 1
+        k, nb = 32, 11
+        ods = np.stack([O.gen_ods(k, 0x3A + b) for b in range(nb)])
+        eds, rr, cr, dah = m.extend_commit_batch(ods)
+        for b in range(nb):
+            rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods[b])
+            assert np.array_equal(eds[b], eds_o) and dah[b].tobytes() == dah_o
+        ods[7, [1, 2]] = ods[7, [2, 1]]
+        with pytest.raises(cda.CdaError) as ei:
+            m.extend_commit_batch(ods, want_eds=False)
+        assert (ei.value.code, ei.value.block) == (-5, 7)
+    finally:
+        m.close()
+
+
 def test_batch_k128_push_error_block(ctx):
     """A push-order error in one block of a batch names that block, axis, index and leaf."""
     from cda import CdaError
@@ -447,29 +508,49 @@ def test_compute_eds_honours_custom_tree_constructor(ctx):
     assert sq.row_roots() == ref.row_roots() and sq.col_roots() == ref.col_roots()
 
 
-def test_device_and_sync_calls_share_the_workspace(ctx):
+_WORKSPACE_SCRIPT = r"""
+import sys
+import numpy as np
+import torch  # first: libcda then resolves HIP through torch's runtime, as in bench.py
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import cda
+import oracle_lib as O
+ctx = cda.Context(0)
+k, B = 32, 8
+w = 2 * k
+ods = np.stack([O.gen_ods(k, 900 + b) for b in range(B)])
+dev = torch.device("cuda", 0)
+d_ods = torch.from_numpy(ods).to(dev)
+d_eds = torch.empty((B, w * w, 512), dtype=torch.uint8, device=dev)
+d_roots = torch.empty((B, 2 * w, 96), dtype=torch.uint8, device=dev)
+d_dah = torch.empty((B, 32), dtype=torch.uint8, device=dev)
+d_status = torch.empty((B,), dtype=torch.int64, device=dev)
+s = torch.cuda.Stream(dev)
+other = O.gen_ods(64, 77)
+dah_other = O.extend_commit(other)[4]
+for _ in range(3):
+    ctx.extend_commit_device(k, B, d_ods.data_ptr(), d_eds.data_ptr(), d_roots.data_ptr(), d_dah.data_ptr(),
+                             d_status.data_ptr(), s.cuda_stream)
+    assert ctx.extend_commit(other)[3] == dah_other  # synchronous, on the ctx's own stream
+s.synchronize()
+for b in range(B):
+    assert d_dah[b].cpu().numpy().tobytes() == O.extend_commit(ods[b])[4], b
+print("workspace ok")
+"""
+
+
+def test_device_and_sync_calls_share_the_workspace():
     """cda_extend_commit_device enqueues on the caller's stream and uses the ctx workspace; a
-    synchronous call issued right after must not overwrite it before the device call's kernels ran."""
-    import torch
-    k, B = 32, 8
-    w = 2 * k
-    ods = np.stack([O.gen_ods(k, 900 + b) for b in range(B)])
-    dev = torch.device("cuda", 0)
-    d_ods = torch.from_numpy(ods).to(dev)
-    d_eds = torch.empty((B, w * w, 512), dtype=torch.uint8, device=dev)
-    d_roots = torch.empty((B, 2 * w, 96), dtype=torch.uint8, device=dev)
-    d_dah = torch.empty((B, 32), dtype=torch.uint8, device=dev)
-    d_status = torch.empty((B,), dtype=torch.int64, device=dev)
-    s = torch.cuda.Stream(dev)
-    other = O.gen_ods(64, 77)
-    _, _, _, dah_other = O.extend_commit(other)
-    for _ in range(3):
-        ctx.extend_commit_device(k, B, d_ods.data_ptr(), d_eds.data_ptr(), d_roots.data_ptr(), d_dah.data_ptr(),
-                                 d_status.data_ptr(), s.cuda_stream)
-        assert ctx.extend_commit(other)[3] == dah_other  # synchronous, on the ctx's own stream
-    s.synchronize()
-    for b in range(B):
-        assert d_dah[b].cpu().numpy().tobytes() == O.extend_commit(ods[b])[4]
+    synchronous call issued right after must not overwrite it before the device call's kernels ran.
+    (Own process: torch must be imported before libcda there, as bench.py does.)"""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "celestia-app_amd")
+    out = subprocess.run([sys.executable, "-c", _WORKSPACE_SCRIPT, pkg, here], capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0 and "workspace ok" in out.stdout, out.stderr[-3000:]
 
 
 def test_axis_root_order_error_wins_over_push_past(ctx):
