@@ -265,6 +265,13 @@ def host_path_measure(ctx, k, nblocks=48, reps=3):
         "with_eds": round(best_of(lambda: ctx.extend_commit(one, want_eds=True)) * 1e3, 3)}
     pin_in.free()
     pin_out.free()
+    import torch
+    h = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
+    d = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+    el_h2d = best_of(lambda: (d.copy_(h, non_blocking=True), torch.cuda.synchronize()))
+    el_d2h = best_of(lambda: (h.copy_(d, non_blocking=True), torch.cuda.synchronize()))
+    out["pcie_copy_gbs"] = {"h2d": round(h.numel() / el_h2d / 1e9, 1), "d2h": round(h.numel() / el_d2h / 1e9, 1),
+                            "note": "256 MiB pinned<->device copy (torch), the link's ceiling for this path"}
     out["note"] = (f"{nblocks} k={k} blocks per call (8 MiB in, + 32 MiB EDS out per block), output reused; bound: "
                    "PCIe Gen5 x16 (~50 GB/s per direction measured by hipMemcpy), H2D for roots_only, D2H with_eds")
     return out
