@@ -12,14 +12,16 @@
 //     *rsmt2d.ExtendedDataSquare, so da.NewDataAvailabilityHeader, Hash and every caller stay unchanged
 //     (../patches/0002-da-ExtendShares-rocm-fast-path.patch routes da.ExtendShares here under -tags rocm).
 //
-// Build: CGO_ENABLED=1 go build -tags rocm (the reference Dockerfile sets CGO_ENABLED=0, Dockerfile:17).
+// Build (go/README.md): copy this directory to pkg/cda, then
+//   CGO_ENABLED=1 CGO_CFLAGS=-I<engine>/include \
+//   CGO_LDFLAGS="-L<engine>/celestia-app_amd/cda -Wl,-rpath,<engine>/celestia-app_amd/cda" go build -tags rocm ./...
+// (the reference Dockerfile sets CGO_ENABLED=0, Dockerfile:17).
 // The cgo rules hold: only byte buffers without Go pointers cross the boundary and libcda keeps no pointer
 // after a call returns.
 package cda
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../include
-#cgo LDFLAGS: -L${SRCDIR}/../../celestia-app_amd/cda -lcda -Wl,-rpath,${SRCDIR}/../../celestia-app_amd/cda
+#cgo LDFLAGS: -lcda
 #include <stdlib.h>
 #include "cda.h"
 */

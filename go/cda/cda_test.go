@@ -1,0 +1,177 @@
+//go:build rocm
+
+// Tests a maintainer runs where Go, the module cache and a GPU exist (CGO_ENABLED=1 go test -tags rocm
+// ./pkg/cda/): they pin the GPU path against the reference's own CPU code -- rsmt2d.NewLeoRSCodec and
+// wrapper.NewConstructor -- on non-constant data, which the container this engine was built in could not do
+// (no Go toolchain; see DESIGN.md §3).
+package cda_test
+
+import (
+	"bytes"
+	"crypto/sha256"
+	"math/rand"
+	"sort"
+	"testing"
+
+	"github.com/celestiaorg/rsmt2d"
+	"github.com/stretchr/testify/require"
+
+	"github.com/celestiaorg/celestia-app/v2/pkg/cda"
+	"github.com/celestiaorg/celestia-app/v2/pkg/wrapper"
+)
+
+// sortedShares: v0 namespaces (0x00 x 19 ‖ 10 random bytes) ‖ 483 random bytes, sorted (SURVEY.md §8d).
+func sortedShares(r *rand.Rand, n int) [][]byte {
+	s := make([][]byte, n)
+	for i := range s {
+		b := make([]byte, cda.ShareSize)
+		r.Read(b[19:])
+		for j := 0; j < 19; j++ {
+			b[j] = 0
+		}
+		s[i] = b
+	}
+	sort.Slice(s, func(i, j int) bool { return bytes.Compare(s[i], s[j]) < 0 })
+	return s
+}
+
+// constantShares is pkg/da's generateShares (data_availability_header_test.go:247-263).
+func constantShares(n int) [][]byte {
+	ns := append(make([]byte, 19), bytes.Repeat([]byte{1}, 10)...)
+	s := make([][]byte, n)
+	for i := range s {
+		s[i] = append(append([]byte{}, ns...), bytes.Repeat([]byte{0xFF}, cda.ShareSize-len(ns))...)
+	}
+	return s
+}
+
+// rfc6962 is go-square merkle.HashFromByteSlices.
+func rfc6962(items [][]byte) []byte {
+	switch len(items) {
+	case 0:
+		h := sha256.Sum256(nil)
+		return h[:]
+	case 1:
+		h := sha256.Sum256(append([]byte{0}, items[0]...))
+		return h[:]
+	}
+	k := 1
+	for k*2 < len(items) {
+		k *= 2
+	}
+	l, r := rfc6962(items[:k]), rfc6962(items[k:])
+	h := sha256.Sum256(append(append([]byte{1}, l...), r...))
+	return h[:]
+}
+
+func TestExtendSharesReferenceKATs(t *testing.T) {
+	for _, tc := range []struct {
+		k    int
+		want []byte
+	}{ // pkg/da/data_availability_header_test.go:34-68
+		{2, []byte{0xb5, 0x6e, 0x4d, 0x25, 0x1a, 0xc2, 0x66, 0xf4, 0xb9, 0x1c, 0xc5, 0x46, 0x4b, 0x3f, 0xc7, 0xef,
+			0xcb, 0xdc, 0x88, 0x80, 0x64, 0x64, 0x74, 0x96, 0xd1, 0x31, 0x33, 0xf0, 0xdc, 0x65, 0xac, 0x25}},
+		{128, []byte{0xb, 0xd3, 0xab, 0xee, 0xac, 0xfb, 0xb0, 0xb9, 0x2d, 0xfb, 0xda, 0xc4, 0xa1, 0x54, 0x86, 0x8e,
+			0x3c, 0x4e, 0x79, 0x66, 0x6f, 0x7f, 0xcf, 0x6c, 0x62, 0xb, 0xb9, 0xd, 0xd3, 0xa0, 0xdc, 0xf0}},
+	} {
+		eds, err := cda.ExtendShares(constantShares(tc.k * tc.k))
+		require.NoError(t, err)
+		rows, err := eds.RowRoots()
+		require.NoError(t, err)
+		cols, err := eds.ColRoots()
+		require.NoError(t, err)
+		require.Equal(t, tc.want, rfc6962(append(rows, cols...)))
+	}
+}
+
+func TestCodecMatchesLeoRSCodec(t *testing.T) {
+	r := rand.New(rand.NewSource(1))
+	gpu, cpu := cda.NewCodec(), rsmt2d.NewLeoRSCodec()
+	for _, k := range []int{1, 2, 3, 5, 16, 100, 128, 129, 256, 512} { // 2k > 256: GF(2^16)
+		data := make([][]byte, k)
+		for i := range data {
+			data[i] = make([]byte, 512)
+			r.Read(data[i])
+		}
+		want, err := cpu.Encode(data)
+		require.NoError(t, err)
+		got, err := gpu.Encode(data)
+		require.NoError(t, err)
+		require.Equal(t, want, got, "k=%d", k)
+		shards := append(append([][]byte{}, data...), want...)
+		for _, i := range r.Perm(2 * k)[:k] {
+			shards[i] = nil
+		}
+		dec, err := gpu.Decode(append([][]byte{}, shards...))
+		require.NoError(t, err)
+		require.Equal(t, append(append([][]byte{}, data...), want...), dec, "decode k=%d", k)
+	}
+}
+
+func TestExtendSharesMatchesCPUPath(t *testing.T) {
+	r := rand.New(rand.NewSource(2))
+	for _, k := range []int{1, 2, 4, 8, 16, 32, 64, 128, 256} {
+		s := sortedShares(r, k*k)
+		want, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+		require.NoError(t, err)
+		got, err := cda.ExtendShares(s)
+		require.NoError(t, err)
+		require.Equal(t, want.Flattened(), got.Flattened(), "k=%d", k)
+		wr, _ := want.RowRoots()
+		gr, _ := got.RowRoots()
+		wc, _ := want.ColRoots()
+		gc, _ := got.ColRoots()
+		require.Equal(t, wr, gr, "k=%d", k)
+		require.Equal(t, wc, gc, "k=%d", k)
+	}
+}
+
+func TestTreeConstructorMatchesWrapper(t *testing.T) {
+	r := rand.New(rand.NewSource(3))
+	k := 16
+	s := sortedShares(r, k*k)
+	want, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+	require.NoError(t, err)
+	got, err := rsmt2d.ComputeExtendedDataSquare(s, cda.NewCodec(), cda.NewConstructor(uint64(k)))
+	require.NoError(t, err)
+	wr, _ := want.RowRoots()
+	gr, _ := got.RowRoots()
+	require.Equal(t, wr, gr)
+}
+
+func TestRepairMatchesRsmt2d(t *testing.T) {
+	r := rand.New(rand.NewSource(4))
+	k := 64
+	s := sortedShares(r, k*k)
+	full, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+	require.NoError(t, err)
+	rows, _ := full.RowRoots()
+	cols, _ := full.ColRoots()
+	flat := full.Flattened()
+	damaged := make([][]byte, len(flat))
+	for i := range flat {
+		if r.Float64() < 0.55 {
+			damaged[i] = append([]byte{}, flat[i]...)
+		}
+	}
+	ctx, err := cda.Default()
+	require.NoError(t, err)
+	require.NoError(t, cda.Repair(ctx, damaged, rows, cols))
+	require.Equal(t, flat, damaged)
+}
+
+func BenchmarkExtendShares(b *testing.B) {
+	s := sortedShares(rand.New(rand.NewSource(5)), 128*128)
+	b.Run("gpu", func(b *testing.B) {
+		for i := 0; i < b.N; i++ {
+			eds, _ := cda.ExtendShares(s)
+			_, _ = eds.RowRoots()
+		}
+	})
+	b.Run("cpu-reference", func(b *testing.B) {
+		for i := 0; i < b.N; i++ {
+			eds, _ := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(128))
+			_, _ = eds.RowRoots()
+		}
+	})
+}

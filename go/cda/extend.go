@@ -1,0 +1,156 @@
+//go:build rocm
+
+package cda
+
+/*
+#include "cda.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"math"
+
+	"github.com/celestiaorg/rsmt2d"
+)
+
+func isPowerOfTwo(n int) bool { return n > 0 && n&(n-1) == 0 }
+
+// squareSize is da.SquareSize (data_availability_header.go:205-216): next power of two >= ceil(sqrt(len)).
+func squareSize(n int) int {
+	k := int(math.Ceil(math.Sqrt(float64(n))))
+	p := 1
+	for p < k {
+		p <<= 1
+	}
+	return p
+}
+
+// ExtendShares is da.ExtendShares (pkg/da/data_availability_header.go:65-75) in one GPU call: the 2-D Leopard
+// extension, every row and column NMT root (and the DAH) are computed by cda_extend_commit; the EDS comes back as
+// an *rsmt2d.ExtendedDataSquare built by rsmt2d.ImportExtendedDataSquare, whose tree constructor returns the GPU
+// roots on the first RowRoots / ColRoots pass, so da.NewDataAvailabilityHeader needs no hashing.
+func ExtendShares(s [][]byte) (*rsmt2d.ExtendedDataSquare, error) {
+	return ExtendSharesOn(mustDefault(), s)
+}
+
+// ExtendSharesOn is ExtendShares on a given context.
+func ExtendSharesOn(ctx *Context, s [][]byte) (*rsmt2d.ExtendedDataSquare, error) {
+	if !isPowerOfTwo(len(s)) {
+		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", len(s))
+	}
+	flat, n, err := flatten(s)
+	if err != nil {
+		return nil, err
+	}
+	k := squareSize(len(s))
+	w := 2 * k
+	eds := make([]byte, w*w*n)
+	rows := make([]byte, w*NodeSize)
+	cols := make([]byte, w*NodeSize)
+	dah := make([]byte, 32)
+	var info C.cda_err_info
+	rc := C.cda_extend_commit(ctx.c, C.uint32_t(len(s)), C.uint32_t(n), ptr(flat), ptr(eds), ptr(rows), ptr(cols),
+		ptr(dah), &info)
+	if rc != 0 {
+		return nil, toErr(rc, &info)
+	}
+	return importWithRoots(ctx, eds, w, n, rows, cols)
+}
+
+func importWithRoots(ctx *Context, eds []byte, w, n int, rows, cols []byte) (*rsmt2d.ExtendedDataSquare, error) {
+	cache := &rootCache{}
+	cache.roots[0] = split(rows, w)
+	cache.roots[1] = split(cols, w)
+	cache.used[0] = make([]bool, w)
+	cache.used[1] = make([]bool, w)
+	return rsmt2d.ImportExtendedDataSquare(split(eds, w*w), NewCodecOn(ctx), cache.constructor(ctx, uint64(w/2)))
+}
+
+// Block is one extended block of a batch: the EDS and the DAH inputs.
+type Block struct {
+	EDS      *rsmt2d.ExtendedDataSquare
+	RowRoots [][]byte
+	ColRoots [][]byte
+	DataHash []byte // DataAvailabilityHeader.Hash (pkg/da/data_availability_header.go:92-108)
+}
+
+// Multi is cda_multi: one handle over the GPUs of this process (device mask bit d = HIP device d, 0 = all).
+type Multi struct {
+	m *C.cda_multi
+}
+
+// NewMulti opens every device in mask.
+func NewMulti(mask uint32) (*Multi, error) {
+	var m *C.cda_multi
+	if rc := C.cda_multi_init(C.uint32_t(mask), &m); rc != 0 {
+		return nil, toErr(rc, nil)
+	}
+	return &Multi{m: m}, nil
+}
+
+// Close releases every device context.
+func (m *Multi) Close() {
+	if m.m != nil {
+		C.cda_multi_free(m.m)
+		m.m = nil
+	}
+}
+
+// ExtendBlocks extends and commits many independent blocks (k*k shares each, same k), sharded over the devices;
+// with withEDS false only the roots and data hashes come back (ProcessProposal needs nothing else).
+func (m *Multi) ExtendBlocks(blocks [][][]byte, withEDS bool) ([]Block, error) {
+	nb := len(blocks)
+	if nb == 0 {
+		return nil, nil
+	}
+	count := len(blocks[0])
+	if !isPowerOfTwo(count) {
+		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", count)
+	}
+	k := squareSize(count)
+	if k*k != count {
+		return nil, &Error{Code: ErrCodeNotSquare, Axis: -1, Index: -1, Leaf: -1, Block: 0}
+	}
+	w := 2 * k
+	ods := make([]byte, nb*count*ShareSize)
+	for b, s := range blocks {
+		if len(s) != count {
+			return nil, fmt.Errorf("block %d has %d shares, want %d", b, len(s), count)
+		}
+		for i, sh := range s {
+			if len(sh) != ShareSize {
+				return nil, fmt.Errorf("block %d share %d is %d bytes", b, i, len(sh))
+			}
+			copy(ods[(b*count+i)*ShareSize:], sh)
+		}
+	}
+	var eds []byte
+	if withEDS {
+		eds = make([]byte, nb*w*w*ShareSize)
+	}
+	rows := make([]byte, nb*w*NodeSize)
+	cols := make([]byte, nb*w*NodeSize)
+	dah := make([]byte, nb*32)
+	var info C.cda_err_info
+	rc := C.cda_multi_extend_commit_batch(m.m, C.uint32_t(k), C.uint32_t(nb), ptr(ods), ptr(eds), ptr(rows), ptr(cols),
+		ptr(dah), &info)
+	if rc != 0 {
+		return nil, toErr(rc, &info)
+	}
+	ctx := &Context{c: C.cda_multi_context(m.m, 0)}
+	out := make([]Block, nb)
+	for b := range out {
+		r := rows[b*w*NodeSize : (b+1)*w*NodeSize]
+		c := cols[b*w*NodeSize : (b+1)*w*NodeSize]
+		out[b].RowRoots, out[b].ColRoots, out[b].DataHash = split(r, w), split(c, w), dah[b*32:(b+1)*32]
+		if withEDS {
+			sq, err := importWithRoots(ctx, eds[b*w*w*ShareSize:(b+1)*w*w*ShareSize], w, ShareSize, r, c)
+			if err != nil {
+				return nil, err
+			}
+			out[b].EDS = sq
+		}
+	}
+	return out, nil
+}

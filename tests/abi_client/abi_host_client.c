@@ -1,0 +1,114 @@
+/*
+ * abi_host_client.c — a plain C caller of libcda.so that uses the C ABI exactly as the cgo shim in
+ * go/cda does: malloc'd (pageable) host buffers standing in for Go slices, flattened shares, roots as
+ * 90-byte records, error details through cda_err_info.  Built by __graft_entry__.build() (gcc, against
+ * include/cda.h); run by tests/test_abi_client.py on the GPU, which checks its outputs against
+ * tests/golden/oracle_digests.json and mainnet block 408's data_hash.
+ *
+ *   abi_host_client <ods.bin> <k> <out_dir>
+ * writes <out_dir>/{eds,row_roots,col_roots,dah,parity,repaired}.bin and prints one status line.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cda.h"
+
+static int write_file(const char* dir, const char* name, const void* p, size_t n) {
+  char path[4096];
+  snprintf(path, sizeof path, "%s/%s", dir, name);
+  FILE* f = fopen(path, "wb");
+  if (!f) return -1;
+  const size_t w = fwrite(p, 1, n, f);
+  fclose(f);
+  return w == n ? 0 : -1;
+}
+
+static int fail(const char* what, int rc, const cda_err_info* e) {
+  fprintf(stderr, "%s: rc=%d (%s) axis=%d index=%d leaf=%d block=%d\n", what, rc, cda_strerror(rc),
+          e ? e->axis : -1, e ? e->index : -1, e ? e->leaf : -1, e ? e->block : -1);
+  return 1;
+}
+
+int main(int argc, char** argv) {
+  if (argc != 4) {
+    fprintf(stderr, "usage: %s <ods.bin> <k> <out_dir>\n", argv[0]);
+    return 2;
+  }
+  const uint32_t k = (uint32_t)atoi(argv[2]), w = 2 * k, count = k * k;
+  const size_t S = CDA_SHARE_SIZE;
+  uint8_t* ods = malloc((size_t)count * S);
+  FILE* f = fopen(argv[1], "rb");
+  if (!f || fread(ods, 1, (size_t)count * S, f) != (size_t)count * S) {
+    fprintf(stderr, "cannot read %s\n", argv[1]);
+    return 2;
+  }
+  fclose(f);
+  cda_ctx* ctx = NULL;
+  int rc = cda_init(0, &ctx);
+  if (rc) return fail("cda_init", rc, NULL);
+
+  /* da.ExtendShares + NewDataAvailabilityHeader: one call */
+  uint8_t* eds = malloc((size_t)w * w * S);
+  uint8_t* rows = malloc((size_t)w * CDA_NODE_SIZE);
+  uint8_t* cols = malloc((size_t)w * CDA_NODE_SIZE);
+  uint8_t dah[32];
+  cda_err_info err;
+  rc = cda_extend_commit(ctx, count, (uint32_t)S, ods, eds, rows, cols, dah, &err);
+  if (rc) return fail("cda_extend_commit", rc, &err);
+
+  /* rsmt2d.Codec.Encode of ODS row 0 (the same bytes as EDS row 0, columns k..2k-1) */
+  uint8_t* parity = malloc((size_t)k * S);
+  rc = cda_rs_encode(ctx, k, (uint32_t)S, ods, parity);
+  if (rc) return fail("cda_rs_encode", rc, NULL);
+  if (memcmp(parity, eds + (size_t)k * S, (size_t)k * S) != 0) {
+    fprintf(stderr, "codec parity differs from EDS row 0\n");
+    return 1;
+  }
+
+  /* Repair from Q0 alone (the quarter of the square a light node must be able to rebuild from) */
+  uint8_t* damaged = malloc((size_t)w * w * S);
+  uint8_t* present = malloc((size_t)w * w);
+  memcpy(damaged, eds, (size_t)w * w * S);
+  for (uint32_t r = 0; r < w; r++)
+    for (uint32_t c = 0; c < w; c++) {
+      present[r * w + c] = (r < k && c < k) ? 1 : 0;
+      if (!present[r * w + c]) memset(damaged + ((size_t)r * w + c) * S, 0, S);
+    }
+  rc = cda_repair(ctx, k, damaged, present, rows, cols, &err);
+  if (rc) return fail("cda_repair", rc, &err);
+  for (uint32_t i = 0; i < w * w; i++)
+    if (!present[i]) {
+      fprintf(stderr, "cell %u still missing after repair\n", i);
+      return 1;
+    }
+
+  /* batch of three copies through the pipelined host path: same DAH each */
+  uint8_t* ods3 = malloc((size_t)3 * count * S);
+  for (int b = 0; b < 3; b++) memcpy(ods3 + (size_t)b * count * S, ods, (size_t)count * S);
+  uint8_t* rows3 = malloc((size_t)3 * w * CDA_NODE_SIZE);
+  uint8_t* cols3 = malloc((size_t)3 * w * CDA_NODE_SIZE);
+  uint8_t dah3[96];
+  rc = cda_extend_commit_batch(ctx, k, 3, ods3, NULL, rows3, cols3, dah3, &err);
+  if (rc) return fail("cda_extend_commit_batch", rc, &err);
+  for (int b = 0; b < 3; b++)
+    if (memcmp(dah3 + 32 * b, dah, 32) != 0) {
+      fprintf(stderr, "batch block %d DAH differs\n", b);
+      return 1;
+    }
+
+  if (write_file(argv[3], "eds.bin", eds, (size_t)w * w * S) || write_file(argv[3], "row_roots.bin", rows, (size_t)w * CDA_NODE_SIZE) ||
+      write_file(argv[3], "col_roots.bin", cols, (size_t)w * CDA_NODE_SIZE) || write_file(argv[3], "dah.bin", dah, 32) ||
+      write_file(argv[3], "parity.bin", parity, (size_t)k * S) || write_file(argv[3], "repaired.bin", damaged, (size_t)w * w * S)) {
+    fprintf(stderr, "cannot write outputs\n");
+    return 1;
+  }
+  printf("abi_host_client ok k=%u dah=", k);
+  for (int i = 0; i < 32; i++) printf("%02x", dah[i]);
+  printf("\n");
+  cda_free(ctx);
+  free(ods); free(eds); free(rows); free(cols); free(parity); free(damaged); free(present);
+  free(ods3); free(rows3); free(cols3);
+  return 0;
+}
