@@ -327,7 +327,10 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
   const int grp = wg % a.groups_per_blk;
   const int blk = wg / a.groups_per_blk;
   const int cw = grp * 2 + cwi;
-  const long long off = (long long)slice * 512 + u * 32;
+  // lane u owns bytes [16u, 16u+16) and [256+16u, 256+16u+16) of each 512-B share: every 16-B load or
+  // store instruction of the wave covers whole 256-B runs (the bit-slice is byte-position agnostic, so
+  // any fixed byte->lane map works as long as load and store agree)
+  const long long off = (long long)slice * 512 + u * 16;
   const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
   uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
   uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
@@ -339,11 +342,11 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
     const int x = x2_of(w, sw, r, 1);
     if (x < a.k) {
       const uint4* p = reinterpret_cast<const uint4*>(src + x * a.src_sh);
-      const uint4 v0 = p[0], v1 = p[1];
+      const uint4 v0 = p[0], v1 = p[16];
       if (cpy) {
         uint4* q = reinterpret_cast<uint4*>(cpy + x * a.cpy_sh);
         q[0] = v0;
-        q[1] = v1;
+        q[16] = v1;
       }
       E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
       E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
@@ -382,7 +385,7 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
       bitslice8(v, ko);
       uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
       q[0] = make_uint4(v[0], v[1], v[2], v[3]);
-      q[1] = make_uint4(v[4], v[5], v[6], v[7]);
+      q[16] = make_uint4(v[4], v[5], v[6], v[7]);
     }
   }
 }

@@ -31,8 +31,12 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32
 __device__ __forceinline__ uint32_t le_window(uint32_t lo, uint32_t hi, int off) {
   return off == 0 ? lo : __builtin_amdgcn_alignbyte(hi, lo, off);
 }
+// One v_perm_b32 picks bytes off+3, off+2, off+1, off of {hi, lo} (selector byte i = source byte of
+// result byte i; 0-3 = lo, 4-7 = hi): the window and the byte swap in a single 4-cycle instruction
+// instead of v_alignbyte + v_perm (profiles/r02_valu_ubench.txt).
 __device__ __forceinline__ uint32_t be_window(uint32_t lo, uint32_t hi, int off) {
-  return bswap(le_window(lo, hi, off));
+  const uint32_t sel = (uint32_t)(off + 3) | (uint32_t)(off + 2) << 8 | (uint32_t)(off + 1) << 16 | (uint32_t)off << 24;
+  return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
 // Round constants; the unrolled rounds index this constexpr table so each K
