@@ -43,6 +43,10 @@ def kernel_step_bytes(name, k, B):
     NMT levels: read 2 child nodes, write 1 (90 B each); dah: read 4k roots.
     """
     w, S, N = 2 * k, 512, 90
+    if name == "rs_rows_leaf":  # read ODS, write Q0 copy + Q1, top-half leaf nodes
+        return B * (3 * k * k * S + k * w * N)
+    if name == "rs_cols_leaf":  # read the top half, write the bottom half and its leaf nodes
+        return B * (2 * w * k * S + k * w * N)
     if name.endswith("_rows"):
         return B * 3 * k * k * S
     if name.endswith("_cols"):
@@ -181,6 +185,7 @@ def repair_measure(ctx, k=128, survive=0.5, reps=3):
 
 # bench kernel name -> rocprofv3 kernel name in profiles/*_counters.json
 PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "nmt_level1": "nmt_level_kernel<true>", "dah": "dah_kernel",
+             "rs_rows_leaf": "rs_rows_leaf_kernel<7>", "rs_cols_leaf": "rs_cols_leaf_kernel<7>",
              "rs_encode8_rows": "rs_encode8_g2_kernel<7>", "rs_encode8_cols": "rs_encode8_g2_kernel<7>"}
 PMC_BATCH = 128  # scripts/profile.sh profiles the default bench step (B = 128 blocks)
 

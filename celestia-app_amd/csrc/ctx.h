@@ -24,6 +24,8 @@ struct cda_ctx {
   int pipe_chunks = 1;
   // CDA_CHUNK: blocks per sequential chunk on one stream (0 = whole batch at once)
   int chunk_blocks = 0;
+  // CDA_FUSED=1: extension fused with leaf hashing (measured no faster; see rs_kernels.hip)
+  bool fused = false;
   hipStream_t sub[kMaxSub] = {};
   // Workspace ordering across streams: the device-resident entry points enqueue on the caller's
   // stream but use this ctx's workspace (leaf/scratch records).  ws_event marks the end of the

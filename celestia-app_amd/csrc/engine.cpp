@@ -202,6 +202,20 @@ int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ed
 
 int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                          void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
+  if (c->fused && rs_leaf_fusable((int)k)) {
+    // extension fused with leaf hashing: rows (Q0 copy + Q1 + top-half leaves), cols (Q2|Q3 + bottom leaves)
+    if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+    {
+      ProfScope ps(c, "rs_rows_leaf", s);
+      if (launch_rs_rows_leaf(rows_job(k, nblocks, d_ods, d_eds), d_ods, d_eds, bufs0(c, rec_off), d_status, s))
+        return CDA_E_DEVICE;
+    }
+    {
+      ProfScope ps(c, "rs_cols_leaf", s);
+      if (launch_rs_cols_leaf(cols_job(k, nblocks, d_eds), d_eds, bufs0(c, rec_off), s)) return CDA_E_DEVICE;
+    }
+    return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, rec_off);
+  }
   if (int rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s)) return rc;
   return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, rec_off);
 }
@@ -318,6 +332,7 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
   if (const char* e = getenv("CDA_PIPELINE")) c->pipe_chunks = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("CDA_CHUNK")) c->chunk_blocks = std::max(0, atoi(e));
+  if (const char* e = getenv("CDA_FUSED")) c->fused = atoi(e) != 0;
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;

@@ -166,6 +166,29 @@ def test_multi_device_batch():
         m.close()
 
 
+@pytest.mark.parametrize("k", [16, 32, 64, 128])
+def test_fused_extension_leaf_kernels(k, monkeypatch):
+    """CDA_FUSED=1: extension fused with leaf hashing (rows+leaf, cols+leaf kernels) -- same bytes, same
+    push-order error reports."""
+    import cda
+    monkeypatch.setenv("CDA_FUSED", "1")
+    c = cda.Context(0)
+    try:
+        nb = 3
+        ods = np.stack([O.gen_ods(k, 0xF00 + b + k) for b in range(nb)])
+        eds, rr, cr, dah = c.extend_commit_batch(ods)
+        for b in range(nb):
+            rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods[b])
+            assert np.array_equal(eds[b], eds_o) and np.array_equal(rr[b], rr_o) and np.array_equal(cr[b], cr_o)
+            assert dah[b].tobytes() == dah_o
+        ods[1, [k + 2, k + 3]] = ods[1, [k + 3, k + 2]]  # row 1 leaves 2 and 3 swapped
+        with pytest.raises(cda.CdaError) as ei:
+            c.extend_commit_batch(ods)
+        assert (ei.value.code, ei.value.block, ei.value.axis, ei.value.index, ei.value.leaf) == (-5, 1, 0, 1, 3)
+    finally:
+        c.close()
+
+
 def test_batch_k128_push_error_block(ctx):
     """A push-order error in one block of a batch names that block, axis, index and leaf."""
     from cda import CdaError
