@@ -55,6 +55,14 @@ def kernel_step_bytes(name, k, B):
         return B * w * w * (S + N)
     if name == "nmt_level1":
         return B * 2 * w * (w // 2) * 3 * N
+    if name == "nmt_levels_1":  # levels 1-2 in one launch: read the leaves, write levels 1 and 2
+        return B * 2 * w * ((w // 2) * 2 * N + (w // 2) * N + (w // 4) * N)
+    if name == "nmt_levels":  # levels 3..log2(w): read level 2, write every later level
+        n, tot = w // 4, 2 * w * (w // 4) * N
+        while n > 1:
+            tot += 2 * w * (n // 2) * N
+            n //= 2
+        return B * tot
     if name == "nmt_level":  # levels 2..log2(w)
         n, tot = w // 2, 0
         while n > 1:
@@ -185,6 +193,7 @@ def repair_measure(ctx, k=128, survive=0.5, reps=3):
 
 # bench kernel name -> rocprofv3 kernel name in profiles/*_counters.json
 PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "nmt_level1": "nmt_level_kernel<true>", "dah": "dah_kernel",
+             "nmt_levels_1": "nmt_levels_kernel", "nmt_levels": "nmt_levels_kernel",
              "rs_rows_leaf": "rs_rows_leaf_kernel<7>", "rs_cols_leaf": "rs_cols_leaf_kernel<7>",
              "rs_encode8_rows": "rs_encode8_g2_kernel<7>", "rs_encode8_cols": "rs_encode8_g2_kernel<7>"}
 PMC_BATCH = 128  # scripts/profile.sh profiles the default bench step (B = 128 blocks)

@@ -62,6 +62,10 @@ int launch_rs_cols_leaf(const RsJob& cols, const uint8_t* d_eds, void* d_nodes, 
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
                      hipStream_t s);
 int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int nblocks, int level, hipStream_t s);
+// Leaf records -> all 4k roots of nblocks blocks, several levels per launch; d_levels: nblocks x 2w x w
+// records of scratch for the inner levels.  prof_ctx: the cda_ctx for ProfScope (or null).
+int launch_nmt_trees(const void* d_leaves, void* d_levels, void* d_roots, int k, int nblocks, hipStream_t s,
+                     void* prof_ctx);
 int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s);
 // single-axis tree (wrapper.NewConstructor tree of n leaves of 512 B)
 int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,

@@ -174,14 +174,11 @@ int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, u
 // NMT levels + DAH of nblocks blocks whose leaf records are at record offset rec_off.
 int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void* d_dah, hipStream_t s, size_t rec_off) {
   const uint32_t w = 2 * k;
-  const int L = ilog2i(w);
-  void* bufs[2] = {(uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES, (uint8_t*)c->scratch.p + rec_off * CDA_REC_BYTES};
-  for (int level = 1; level <= L; level++) {
-    const void* in = bufs[(level - 1) & 1];
-    void* out = level == L ? d_roots : bufs[level & 1];
-    ProfScope ps(c, level == 1 ? "nmt_level1" : "nmt_level", s);
-    if (launch_nmt_level(in, out, level == 1, (int)k, (int)nblocks, level, s)) return CDA_E_DEVICE;
-  }
+  // inner levels in c->scratch: 2 records per leaf record of the chunk (2w x (w - 2) per block)
+  const int lr0 = launch_nmt_trees((uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES,
+                                   (uint8_t*)c->scratch.p + 2 * rec_off * CDA_REC_BYTES, d_roots, (int)k, (int)nblocks, s,
+                                   c);
+  if (lr0) return lr0 == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   {
     ProfScope ps(c, "dah", s);
     const int lr = launch_dah(d_roots, d_dah, (int)(2 * w), (int)nblocks, s);
@@ -231,7 +228,7 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   const size_t cells = (size_t)nblocks * w * w;
   int rc = ensure(c, c->leaf, cells * CDA_REC_BYTES);
   if (rc) return rc;
-  rc = ensure(c, c->scratch, cells * CDA_REC_BYTES);
+  rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES);  // inner tree levels
   if (rc) return rc;
   if (!c->prof && c->pipe_chunks > 1 && nblocks > 1) {
     // Two-stream software pipeline: stream sub[0] runs the RS phase chunk after chunk,
@@ -614,7 +611,7 @@ int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_root
   int rc;
   if ((rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->roots, roots_b)) || (rc = ensure(c, c->dah, 32)) ||
       (rc = ensure(c, c->status, 8)) || (rc = ensure(c, c->leaf, (size_t)w * w * CDA_REC_BYTES)) ||
-      (rc = ensure(c, c->scratch, (size_t)w * w * CDA_REC_BYTES)))
+      (rc = ensure(c, c->scratch, (size_t)2 * w * w * CDA_REC_BYTES)))
     return rc;
   hipStream_t s = c->stream;
   if (!dev_ok(c, hipMemcpyAsync(c->eds.p, eds, eds_b, hipMemcpyHostToDevice, s), "H2D") ||
@@ -625,13 +622,9 @@ int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_root
     if (launch_leaf_hash((const uint8_t*)c->eds.p, c->leaf.p, (unsigned long long*)c->status.p, (int)k, 1, s))
       return CDA_E_DEVICE;
   }
-  const int L = ilog2i(w);
-  void* bufs[2] = {c->leaf.p, c->scratch.p};
-  for (int level = 1; level <= L; level++) {
-    ProfScope ps(c, "nmt_level", s);
-    if (launch_nmt_level(bufs[(level - 1) & 1], level == L ? c->roots.p : bufs[level & 1], level == 1, (int)k, 1,
-                         level, s))
-      return CDA_E_DEVICE;
+  {
+    const int lr = launch_nmt_trees(c->leaf.p, c->scratch.p, c->roots.p, (int)k, 1, s, c);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   {
     ProfScope ps(c, "dah", s);

@@ -112,7 +112,7 @@ int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods
   if ((rc = ensure(c, c->ods, S * C * ods_blk)) || (rc = ensure(c, c->eds, S * C * eds_blk)) ||
       (rc = ensure(c, c->roots, S * C * rec_blk)) || (rc = ensure(c, c->dah, (size_t)S * C * 32)) ||
       (rc = ensure(c, c->status, (size_t)S * C * 8)) || (rc = ensure(c, c->leaf, (size_t)C * w * w * CDA_REC_BYTES)) ||
-      (rc = ensure(c, c->scratch, (size_t)C * w * w * CDA_REC_BYTES)))
+      (rc = ensure(c, c->scratch, (size_t)2 * C * w * w * CDA_REC_BYTES)))
     return rc;
   std::vector<uint8_t> recs((size_t)nblocks * rec_blk);
   std::vector<uint64_t> st(nblocks);

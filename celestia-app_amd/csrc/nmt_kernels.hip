@@ -18,6 +18,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "cda_internal.h"
 #include "nmt_dev.h"
 #include "sha256_dev.h"
@@ -75,6 +77,107 @@ __global__ void __launch_bounds__(256) nmt_level_kernel(const uint4* __restrict_
     ib = ia + 1;
   }
   hash_node_mem(in + ia * 6, in + ib * 6, out + (size_t)gid * 6);
+}
+
+// ---------------------------------------------------------------------------
+// Row and column trees of a batch of blocks, M levels per launch.
+//
+// Layout of level l (n_l = w >> l nodes per tree) for block b, in 96-B records:
+//   row tree r, node i :  base + b*blk + row0 + r*row_t + i*row_i
+//   col tree c, node i :  base + b*blk + col0 + c*col_t + i*col_i
+// Leaves (l = 0) are the cell-major leaf records (row_t = w, row_i = 1, col_t = 1, col_i = w); inner
+// levels keep row trees tree-major ([r][i]) and column trees node-major ([i][c]), so that for both
+// kinds the 64 lanes of a wave read 64 adjacent records (row trees: lanes = consecutive i, two
+// children each, 192 contiguous bytes per lane; column trees: lanes = consecutive c) and write 64
+// adjacent records.  The roots land in d_roots[b][0..w) (rows) and [w..2w) (columns).
+//
+// A thread owns one output node at level l_in + M and computes its whole subtree level by level
+// (2^M - 1 nodes, the intermediate levels written to their level buffers and read back by the same
+// thread), so a launch covers M levels: the levels of one block's 4k trees take ceil(log2(2k) / M)
+// launches instead of log2(2k).
+// ---------------------------------------------------------------------------
+struct LevelDesc {
+  uint4* p;
+  unsigned long long blk;  // records per block
+  unsigned row0, row_t, row_i, col0, col_t, col_i;
+};
+struct LevelSet {
+  LevelDesc lv[4];  // levels l_in .. l_in + M (M <= 3)
+};
+
+__device__ __forceinline__ uint4* level_rec(const LevelDesc& d, unsigned b, bool col, unsigned tree, unsigned i) {
+  const unsigned long long off =
+      (unsigned long long)b * d.blk + (col ? d.col0 + tree * d.col_t + i * d.col_i : d.row0 + tree * d.row_t + i * d.row_i);
+  return d.p + off * 6;
+}
+
+__global__ void __launch_bounds__(256) nmt_levels_kernel(LevelSet ls, int log2w, int log2n_out, int M, uint32_t total) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const unsigned w = 1u << log2w;
+  const unsigned per_kind = w << log2n_out;  // output nodes of the row (or column) trees of one block
+  const unsigned b = gid / (2 * per_kind);
+  const unsigned rem = gid - b * 2 * per_kind;
+  const bool col = rem >= per_kind;
+  const unsigned r2 = col ? rem - per_kind : rem;
+  // row trees: node index fastest; column trees: column fastest
+  const unsigned tree = col ? (r2 & (w - 1)) : (r2 >> log2n_out);
+  const unsigned j = col ? (r2 >> log2w) : (r2 & ((1u << log2n_out) - 1));
+  for (int q = 1; q <= M; q++) {
+    const unsigned cnt = 1u << (M - q);  // nodes of this subtree at level l_in + q
+    for (unsigned t = 0; t < cnt; t++) {
+      const unsigned i = j * cnt + t;
+      hash_node_mem(level_rec(ls.lv[q - 1], b, col, tree, 2 * i), level_rec(ls.lv[q - 1], b, col, tree, 2 * i + 1),
+                    level_rec(ls.lv[q], b, col, tree, i));
+    }
+    // the next level reads what this thread just stored
+    if (q < M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// Leaf records -> roots of all 4k trees of nblocks blocks.  d_levels holds the inner levels
+// (2w x (w - 2) records per block at most); M = 2 levels per launch (the last launch may take 1 or 3).
+int launch_nmt_trees(const void* d_leaves, void* d_levels, void* d_roots, int k, int nblocks, hipStream_t s,
+                     void* prof_ctx) {
+  const int w = 2 * k;
+  int L = 0;
+  while ((1 << L) < w) L++;
+  if ((1 << L) != w || L < 1) return -2;
+  auto desc = [&](int l) {
+    LevelDesc d{};
+    const unsigned n = (unsigned)(w >> l);
+    if (l == 0) {
+      d.p = (uint4*)d_leaves;
+      d.blk = (unsigned long long)w * w;
+      d.row0 = 0, d.row_t = w, d.row_i = 1, d.col0 = 0, d.col_t = 1, d.col_i = w;
+    } else if (l == L) {
+      d.p = (uint4*)d_roots;
+      d.blk = 2ull * w;
+      d.row0 = 0, d.row_t = 1, d.row_i = 0, d.col0 = w, d.col_t = 1, d.col_i = 0;
+    } else {
+      unsigned long long off = 0;  // levels 1 .. l-1 before this one
+      for (int q = 1; q < l; q++) off += 2ull * w * (w >> q);
+      d.p = (uint4*)d_levels + off * (unsigned long long)nblocks * 6;
+      d.blk = 2ull * w * n;
+      d.row0 = 0, d.row_t = n, d.row_i = 1, d.col0 = w * n, d.col_t = 1, d.col_i = w;
+    }
+    return d;
+  };
+  for (int l_in = 0; l_in < L;) {
+    int M = std::min(2, L - l_in);
+    if (L - l_in == 3) M = 3;  // finish with one 3-level launch rather than 2 + 1
+    LevelSet ls{};
+    for (int q = 0; q <= M; q++) ls.lv[q] = desc(l_in + q);
+    const int log2n_out = L - (l_in + M);
+    const uint32_t total = (uint32_t)nblocks * 2u * ((uint32_t)w << log2n_out);
+    {
+      ProfScope ps(prof_ctx, l_in == 0 ? "nmt_levels_1" : "nmt_levels", s);
+      hipLaunchKernelGGL(nmt_levels_kernel, dim3((total + 255) / 256), dim3(256), 0, s, ls, L, log2n_out, M, total);
+    }
+    if (hipGetLastError() != hipSuccess) return -1;
+    l_in += M;
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
