@@ -47,13 +47,20 @@ EXPORTS = [
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
     "cda_blob_commitments", "cda_merkle_roots", "cda_extend_commit_nodes", "cda_share_inclusion_proof",
     "cda_host_alloc", "cda_host_free", "cda_multi_init", "cda_multi_free", "cda_multi_device_count",
-    "cda_multi_context", "cda_multi_extend_commit_batch",
+    "cda_multi_context", "cda_multi_extend_commit_batch", "cda_build_ods_device", "cda_construct_extend_commit",
 ]
 
 
 class ErrInfo(ctypes.Structure):
     _fields_ = [("code", ctypes.c_int32), ("axis", ctypes.c_int32), ("index", ctypes.c_int32),
                 ("leaf", ctypes.c_int32), ("block", ctypes.c_int32)]
+
+
+class ShareSegment(ctypes.Structure):
+    """cda_share_segment (include/cda.h): one run of shares of a square plan."""
+    _fields_ = [("kind", ctypes.c_uint32), ("first_share", ctypes.c_uint32), ("nshares", ctypes.c_uint32),
+                ("share_version", ctypes.c_uint32), ("data_off", ctypes.c_uint64), ("data_len", ctypes.c_uint64),
+                ("reserved_off", ctypes.c_uint32), ("ns", ctypes.c_uint8 * 29), ("pad_", ctypes.c_uint8 * 3)]
 
 
 class ShareProofInfo(ctypes.Structure):
@@ -119,6 +126,8 @@ def lib():
                 "cda_multi_device_count": (I32, [P]),
                 "cda_multi_context": (P, [P, I32]),
                 "cda_multi_extend_commit_batch": (I32, [P, U32, U32, P, P, P, P, P, P]),
+                "cda_build_ods_device": (I32, [P, U32, U32, P, P, U64, P, U32, P, P]),
+                "cda_construct_extend_commit": (I32, [P, U32, U32, P, P, U64, P, U32, P, P, P, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)
@@ -211,6 +220,24 @@ class Context:
                                            ctypes.byref(err))
         _check(rc, err, self)
         return eds, rr, cr, dah
+
+    def construct_extend_commit(self, k, segs, want_ods=False, want_eds=True):
+        """square.Construct + ExtendShares + NewDataAvailabilityHeader from a square plan (cda.square.plan):
+        the shares are assembled on the device (cda_construct_extend_commit).  -> (ods, eds, rr, cr, dah)."""
+        from .square import device_plan
+        recs, data, reserved = device_plan(segs)
+        w = 2 * k
+        ods = np.empty((k * k, SHARE_SIZE), np.uint8) if want_ods else None
+        eds = np.empty((w * w, SHARE_SIZE), np.uint8) if want_eds else None
+        rr = np.empty((w, NODE_SIZE), np.uint8)
+        cr = np.empty((w, NODE_SIZE), np.uint8)
+        dah = np.empty(32, np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_construct_extend_commit(self._h, k, len(recs), ctypes.cast(recs, ctypes.c_void_p), _p(data),
+                                               sum(r.data_len for r in recs), _p(reserved), len(reserved), _p(ods),
+                                               _p(eds), _p(rr), _p(cr), _p(dah), ctypes.byref(err))
+        _check(rc, err, self)
+        return ods, eds, rr, cr, dah.tobytes()
 
     def extend_commit_device(self, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, stream=None):
         rc = lib().cda_extend_commit_device(self._h, k, nblocks, ctypes.c_void_p(d_ods), ctypes.c_void_p(d_eds),

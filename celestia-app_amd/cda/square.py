@@ -140,25 +140,37 @@ def compact_shares_needed(sequence_len):
     return 1 + math.ceil((sequence_len - FIRST_COMPACT_SHARE_CONTENT_SIZE) / CONTINUATION_COMPACT_SHARE_CONTENT_SIZE)
 
 
-def compact_shares(ns, units):
-    """CompactShareSplitter: varint-delimited units, sequence length, reserved bytes (shares.md:61-80)."""
+def compact_layout(units):
+    """The varint-delimited sequence of `units` and, per compact share, its reserved bytes value: the offset in
+    the share of the first unit that starts in it, 0 if none (shares.md:61-80)."""
     seq = b"".join(varint(len(u)) + u for u in units)
     starts, off = [], 0
     for u in units:
         starts.append(off)
         off += len(varint(len(u))) + len(u)
-    out, pos = [], 0
+    reserved, pos = [], 0
     for s in range(compact_shares_needed(len(seq))):
+        first = s == 0
+        cap = FIRST_COMPACT_SHARE_CONTENT_SIZE if first else CONTINUATION_COMPACT_SHARE_CONTENT_SIZE
+        data_start = NS + 1 + (4 if first else 0) + 4
+        lo, hi = pos, pos + cap
+        first_unit = next((st for st in starts if lo <= st < hi), None)
+        reserved.append(0 if first_unit is None else data_start + (first_unit - lo))
+        pos = hi
+    return seq, reserved
+
+
+def compact_shares(ns, units):
+    """CompactShareSplitter: varint-delimited units, sequence length, reserved bytes (shares.md:61-80)."""
+    seq, reserved = compact_layout(units)
+    out, pos = [], 0
+    for s, resv in enumerate(reserved):
         first = s == 0
         header = ns + bytes([1 if first else 0]) + (len(seq).to_bytes(4, "big") if first else b"")
         cap = FIRST_COMPACT_SHARE_CONTENT_SIZE if first else CONTINUATION_COMPACT_SHARE_CONTENT_SIZE
-        data_start = len(header) + 4
-        lo, hi = pos, pos + cap
-        first_unit = next((st for st in starts if lo <= st < hi), None)
-        reserved = 0 if first_unit is None else data_start + (first_unit - lo)
-        share = header + reserved.to_bytes(4, "big") + seq[lo:hi]
+        share = header + resv.to_bytes(4, "big") + seq[pos:pos + cap]
         out.append(share + bytes(SHARE - len(share)))
-        pos = hi
+        pos += cap
     return out
 
 
@@ -183,12 +195,11 @@ def padding_share(ns):
 
 
 # ---- square.Construct ----------------------------------------------------------------------------
-def construct(txs, max_square_size=appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND,
-              subtree_root_threshold=appconsts.SUBTREE_ROOT_THRESHOLD, square_size_upper_bound=None):
-    """square.Construct(txs, maxSquareSize, subtreeRootThreshold) -> (square size k, k*k shares, layout info).
-
-    square_size_upper_bound sizes the PFB share-index reservation (defaults to max_square_size).
-    """
+def plan(txs, max_square_size=appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND,
+         subtree_root_threshold=appconsts.SUBTREE_ROOT_THRESHOLD, square_size_upper_bound=None):
+    """square.Construct's layout (go-square v1.0.1) without the share bytes: (k, segments, info).  A segment is
+    a run of shares of one sequence: compact (TRANSACTION / PAY_FOR_BLOB units), sparse (one blob) or padding;
+    render() turns them into shares on the host, cda_construct_extend_commit on the device."""
     upper = square_size_upper_bound or max_square_size
     normal, pfbs, blobs = [], [], []
     for raw in txs:
@@ -216,7 +227,6 @@ def construct(txs, max_square_size=appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND,
     blobs.sort(key=lambda b: b["blob"]["ns"])  # stable: PFB order within a namespace
     non_reserved_start = tx_shares + pfb_reserved
     cursor = end_last = non_reserved_start
-    blob_out = []
     for i, b in enumerate(blobs):
         cursor = next_share_index(cursor, b["n"], subtree_root_threshold)
         if i == 0:
@@ -225,22 +235,89 @@ def construct(txs, max_square_size=appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND,
         if pad > b["max_pad"]:
             raise SquareError("blob padding exceeds its subtree width")
         pfbs[b["pfb"]]["idx"][b["j"]] = cursor
-        if i > 0:
-            blob_out += [padding_share(blobs[i - 1]["blob"]["ns"])] * pad
-        blob_out += sparse_shares(b["blob"]["ns"], b["blob"]["data"], b["blob"]["share_version"])
+        b["start"] = cursor
         cursor += b["n"]
         end_last = cursor
-    square = compact_shares(TX_NAMESPACE, normal)
-    pfb_sh = compact_shares(PAY_FOR_BLOB_NAMESPACE, [marshal_index_wrapper(p["tx"], p["idx"]) for p in pfbs])
-    if len(pfb_sh) > pfb_reserved:
+    pfb_units = [marshal_index_wrapper(p["tx"], p["idx"]) for p in pfbs]
+    if compact_shares_needed(sum(len(varint(len(u))) + len(u) for u in pfb_units)) > pfb_reserved:
         raise SquareError("PFB shares exceed their reservation")
-    square += pfb_sh
-    if blob_out:
-        square += [padding_share(PRIMARY_RESERVED_PADDING_NAMESPACE)] * (non_reserved_start - len(square))
-        square += blob_out
-    square += [padding_share(TAIL_PADDING_NAMESPACE)] * (ss * ss - len(square))
+    # the square as segments (row-major share runs): compact txs, compact PFBs, reserved padding up to the
+    # first blob, blobs with namespace padding between them, tail padding
+    segs, n = [], 0
+
+    def add(kind, count, ns, payload=None):
+        nonlocal n
+        if count > 0:
+            segs.append({"kind": kind, "first": n, "n": count, "ns": ns, "payload": payload})
+            n += count
+    add("compact", tx_shares, TX_NAMESPACE, normal)
+    add("compact", compact_shares_needed(sum(len(varint(len(u))) + len(u) for u in pfb_units)),
+        PAY_FOR_BLOB_NAMESPACE, pfb_units)
+    pfb_count = n - tx_shares
+    if blobs:
+        add("padding", non_reserved_start - n, PRIMARY_RESERVED_PADDING_NAMESPACE)
+        prev_end = None
+        for b in blobs:
+            start = b["start"]
+            if prev_end is not None:
+                add("padding", start - prev_end, prev_ns)
+            add("sparse", b["n"], b["blob"]["ns"], b["blob"])
+            prev_end, prev_ns = start + b["n"], b["blob"]["ns"]
+    add("padding", ss * ss - n, TAIL_PADDING_NAMESPACE)
     info = {"normal_txs": len(normal), "pfbs": len(pfbs), "blobs": len(blobs), "tx_shares": tx_shares,
-            "pfb_shares": len(pfb_sh), "pfb_reserved": pfb_reserved,
+            "pfb_shares": pfb_count, "pfb_reserved": pfb_reserved,
             "first_blob": non_reserved_start if blobs else None, "current_size": current,
             "pfb_share_indexes": [p["idx"] for p in pfbs]}
-    return ss, square, info
+    return ss, segs, info
+
+
+def render(segs):
+    """Host bytes of a plan (shares.ToBytes order): list of 512-byte shares."""
+    out = []
+    for sg in segs:
+        if sg["kind"] == "compact":
+            out += compact_shares(sg["ns"], sg["payload"])
+        elif sg["kind"] == "sparse":
+            out += sparse_shares(sg["ns"], sg["payload"]["data"], sg["payload"]["share_version"])
+        else:
+            out += [padding_share(sg["ns"])] * sg["n"]
+    return out
+
+
+def construct(txs, max_square_size=appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND,
+              subtree_root_threshold=appconsts.SUBTREE_ROOT_THRESHOLD, square_size_upper_bound=None):
+    """square.Construct(txs, maxSquareSize, subtreeRootThreshold) -> (square size k, k*k shares, layout info).
+
+    square_size_upper_bound sizes the PFB share-index reservation (defaults to max_square_size).
+    """
+    ss, segs, info = plan(txs, max_square_size, subtree_root_threshold, square_size_upper_bound)
+    return ss, render(segs), info
+
+
+SEG_KIND = {"compact": 0, "sparse": 1, "padding": 2}  # CDA_SEG_* (include/cda.h)
+
+
+def device_plan(segs):
+    """The plan as cda_share_segment records + payload bytes + compact reserved offsets (numpy arrays)."""
+    import numpy as np
+    from ._native import ShareSegment
+    recs = (ShareSegment * len(segs))()
+    data, reserved, off = [], [], 0
+    for i, sg in enumerate(segs):
+        r = recs[i]
+        r.kind, r.first_share, r.nshares, r.share_version = SEG_KIND[sg["kind"]], sg["first"], sg["n"], 0
+        r.ns[:] = list(sg["ns"])
+        if sg["kind"] == "compact":
+            seq, resv = compact_layout(sg["payload"])
+            r.reserved_off = len(reserved)
+            reserved += resv
+            payload = seq
+        elif sg["kind"] == "sparse":
+            payload = sg["payload"]["data"]
+            r.share_version = sg["payload"]["share_version"]
+        else:
+            payload = b""
+        r.data_off, r.data_len = off, len(payload)
+        data.append(payload)
+        off += len(payload)
+    return recs, np.frombuffer(b"".join(data) or b"\0", np.uint8), np.array(reserved or [0], np.uint32)

@@ -104,6 +104,10 @@ int launch_blob_mountain_level(const BlobDesc* d_desc, int nblobs, void* d_recs,
 int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t* d_off, int nsets, int max_set,
                        void* d_out, void* d_nodes_out, hipStream_t s);
 
+// ODS of a share plan (square_kernels.hip), one thread per 16-B word; -2: empty plan
+int launch_build_ods(const cda_share_segment* d_segs, int nseg, const uint8_t* d_data, const uint32_t* d_reserved,
+                     uint32_t nshares, void* d_ods, hipStream_t s);
+
 // profiling hook implemented by the engine
 struct ProfScope {
   void* ctx;

@@ -44,7 +44,7 @@ struct cda_ctx {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf ods, eds, leaf, scratch, roots, dah, status, host_status;
+  Buf ods, eds, leaf, scratch, roots, dah, status, host_status, plan, payload;
   // profiling
   bool prof = false;
   struct Pending {

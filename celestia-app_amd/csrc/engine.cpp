@@ -350,7 +350,7 @@ void cda_free(cda_ctx* c) {
     Lock l(c);
     (void)hipStreamSynchronize(c->stream);
     flush_profile(c);
-    for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status})
+    for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status, &c->plan, &c->payload})
       if (b->p) (void)hipFree(b->p);
     if (c->host_status.p) (void)hipHostFree(c->host_status.p);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);

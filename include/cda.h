@@ -242,6 +242,35 @@ int cda_share_inclusion_proof(cda_ctx* ctx, uint32_t count, uint32_t share_len, 
                               uint8_t* aunts, int32_t* nmt_start, int32_t* nmt_end, int32_t* nmt_count,
                               uint8_t* nmt_nodes, uint8_t* data_root, cda_err_info* err);
 
+/* ---- square construction on the device (go-square square.Construct + shares.ToBytes) ---- */
+/* The step before the DA path (app/prepare_proposal.go:54,65, app/process_proposal.go:121,137): the
+ * host plans the layout -- which sequence or blob goes where, the PFB share indexes, the compact
+ * reserved offsets -- as share segments; libcda writes the k*k shares straight into device memory
+ * (specs/src/specs/shares.md) and, in cda_construct_extend_commit, extends and commits them.  Segments
+ * are sorted by first_share and tile [0, k*k) exactly. */
+enum { CDA_SEG_COMPACT = 0, CDA_SEG_SPARSE = 1, CDA_SEG_PADDING = 2 };
+typedef struct {
+  uint32_t kind;          /* CDA_SEG_* */
+  uint32_t first_share;   /* row-major ODS index of the segment's first share */
+  uint32_t nshares;
+  uint32_t share_version; /* info byte = share_version << 1 | sequence start */
+  uint64_t data_off;      /* COMPACT: varint-delimited sequence, SPARSE: blob data, in `data` */
+  uint64_t data_len;      /* sequence length written in the first share (0 for padding) */
+  uint32_t reserved_off;  /* COMPACT: index in `reserved` of the segment's first share */
+  uint8_t ns[29];         /* namespace (version byte ‖ 28-byte ID) */
+  uint8_t pad_[3];
+} cda_share_segment;
+/* Builds the ODS (k*k*512 bytes) of the plan into device memory d_ods on `stream` (asynchronous). */
+int cda_build_ods_device(cda_ctx* ctx, uint32_t k, uint32_t nseg, const cda_share_segment* segs, const uint8_t* data,
+                         uint64_t data_len, const uint32_t* reserved, uint32_t nreserved, void* d_ods, void* stream);
+/* square.Construct + shares.ToBytes + da.ExtendShares + NewDataAvailabilityHeader in one call from a
+ * host plan: only the payload bytes (sequences and blobs) cross PCIe.  Outputs as cda_extend_commit
+ * (ods_or_null additionally receives the k*k shares). */
+int cda_construct_extend_commit(cda_ctx* ctx, uint32_t k, uint32_t nseg, const cda_share_segment* segs,
+                                const uint8_t* data, uint64_t data_len, const uint32_t* reserved, uint32_t nreserved,
+                                uint8_t* ods_or_null, uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots,
+                                uint8_t* dah, cda_err_info* err);
+
 /* ---- instrumentation ----------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed by HIP events on its own
  * stream and per-kernel total time / launch counts are accumulated. */

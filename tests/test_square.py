@@ -62,3 +62,57 @@ def test_construct_and_extend_on_gpu(ctx):
     txs, data_hash = mainnet_txs()
     _, shares, _ = S.construct(txs, 128, 64)
     assert da.new_data_availability_header(da.extend_shares(shares)).hash() == data_hash
+
+
+def _blob_tx(rng, nblobs):
+    """A BlobTx (blob.MarshalBlobTx: tx=1, blobs=2, type_id=3 "BLOB") with random v0 namespaces and sizes."""
+    tx = bytes(rng.integers(0, 256, int(rng.integers(50, 400)), dtype=np.uint8))
+    out = b"\x0a" + S.varint(len(tx)) + tx
+    for _ in range(nblobs):
+        # v0 ID: 18 zero bytes then 10 bytes, above the reserved namespaces (first byte non-zero)
+        ns_id = bytes(18) + bytes([int(rng.integers(1, 256))]) + bytes(rng.integers(0, 256, 9, dtype=np.uint8))
+        data = bytes(rng.integers(0, 256, int(rng.integers(1, 6000)), dtype=np.uint8))
+        blob = b"\x0a" + S.varint(len(ns_id)) + ns_id + b"\x12" + S.varint(len(data)) + data
+        out += b"\x12" + S.varint(len(blob)) + blob
+    return out + b"\x1a\x04BLOB"
+
+
+def _random_txs(seed, n_normal, n_blob_txs):
+    rng = np.random.default_rng(seed)
+    txs = [bytes(rng.integers(0, 256, int(rng.integers(100, 900)), dtype=np.uint8)) for _ in range(n_normal)]
+    txs += [_blob_tx(rng, int(rng.integers(1, 4))) for _ in range(n_blob_txs)]
+    return txs
+
+
+def test_plan_tiles_the_square():
+    for seed in range(4):
+        ss, segs, _ = S.plan(_random_txs(seed, 20, 15), 128, 64)
+        assert segs[0]["first"] == 0 and sum(sg["n"] for sg in segs) == ss * ss
+        assert all(a["first"] + a["n"] == b["first"] for a, b in zip(segs, segs[1:]))
+        recs, data, reserved = S.device_plan(segs)
+        for r, sg in zip(recs, segs):
+            if sg["kind"] == "compact":
+                assert S.compact_shares_needed(r.data_len) == sg["n"]
+
+
+@pytest.mark.gpu
+def test_device_square_mainnet_block_408(ctx):
+    """cda_construct_extend_commit: block 408's plan assembled on the GPU gives the reference ODS and data_hash."""
+    txs, data_hash = mainnet_txs()
+    ss, segs, _ = S.plan(txs, 128, 64)
+    ods, eds, rr, cr, dah = ctx.construct_extend_commit(ss, segs, want_ods=True)
+    assert np.array_equal(ods, np.load(os.path.join(GOLDEN, "mainnet_h408.npz"))["ods"])
+    assert dah == data_hash
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n_normal,n_blob", [(1, 0, 0), (2, 3, 0), (3, 0, 2), (4, 40, 30), (5, 200, 120)])
+def test_device_square_matches_host(ctx, seed, n_normal, n_blob):
+    """Random normal txs and multi-blob BlobTxs: the device-built ODS equals the host render byte for byte and the
+    roots / DAH equal the oracle's on that ODS."""
+    ss, segs, _ = S.plan(_random_txs(seed, n_normal, n_blob), 128, 64)
+    host = np.frombuffer(b"".join(S.render(segs)), np.uint8).reshape(-1, 512)
+    ods, eds, rr, cr, dah = ctx.construct_extend_commit(ss, segs, want_ods=True)
+    assert np.array_equal(ods, host)
+    rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(host)
+    assert rc == 0 and dah == dah_o and np.array_equal(eds, eds_o)
