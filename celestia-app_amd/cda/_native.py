@@ -303,16 +303,23 @@ class Context:
         _check(rc, err, self)
         return root.tobytes()
 
-    def repair(self, eds, present, row_roots, col_roots):
-        rc, eds, pres, err = self.repair_status(eds, present, row_roots, col_roots)
+    def repair(self, eds, present, row_roots, col_roots, inplace=False):
+        rc, eds, pres, err = self.repair_status(eds, present, row_roots, col_roots, inplace)
         _check(rc, err, self)
         return eds, pres
 
-    def repair_status(self, eds, present, row_roots, col_roots):
+    def repair_status(self, eds, present, row_roots, col_roots, inplace=False):
         """cda_repair without raising: (rc, eds, present, err) where eds/present hold the square as far as
-        it was repaired (rsmt2d leaves the square 'most repaired prior to the Byzantine axis')."""
-        eds = np.ascontiguousarray(eds, np.uint8).copy()
-        pres = np.ascontiguousarray(present, np.uint8).copy()
+        it was repaired (rsmt2d leaves the square 'most repaired prior to the Byzantine axis').  inplace=True
+        repairs the caller's C-contiguous uint8 arrays themselves (as the C ABI does) instead of copies."""
+        if inplace:
+            if not (isinstance(eds, np.ndarray) and eds.dtype == np.uint8 and eds.flags.c_contiguous
+                    and isinstance(present, np.ndarray) and present.dtype == np.uint8 and present.flags.c_contiguous):
+                raise CdaError(E_ARG, "inplace repair needs C-contiguous uint8 arrays")
+            pres = present
+        else:
+            eds = np.ascontiguousarray(eds, np.uint8).copy()
+            pres = np.ascontiguousarray(present, np.uint8).copy()
         w = len(row_roots)
         if eds.shape[0] != w * w or eds.size != w * w * SHARE_SIZE or pres.size != w * w:
             raise CdaError(E_ARG, "eds must be (2k)^2 x 512 bytes and present (2k)^2 flags")

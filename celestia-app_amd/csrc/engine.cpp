@@ -902,26 +902,43 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
   long long* d_off = (long long*)c->dah.p;
   long long* d_stride = d_off + trees_cap;
   uint8_t* d_pres = (uint8_t*)(d_stride + trees_cap);
+  // present-cell counts per row / column of P, kept in step with it (the replay below is O(w^2) per sweep)
+  std::vector<int> pcnt[2] = {std::vector<int>(w, 0), std::vector<int>(w, 0)};
+  for (int r = 0; r < w; r++)
+    for (int q = 0; q < w; q++)
+      if (P[(size_t)r * w + q]) {
+        pcnt[CDA_AXIS_ROW][r]++;
+        pcnt[CDA_AXIS_COL][q]++;
+      }
   for (;;) {
     // replay one sweep on the presence bitmap
     std::vector<uint8_t> Ps = P;
+    std::vector<int> scnt[2] = {pcnt[0], pcnt[1]};
     std::vector<Op> ops;
     bool solved = true, progress = false;
     for (int i = 0; i < w; i++) {
       for (int axis = 0; axis < 2; axis++) {
-        const int n = count(Ps, axis, i, -1);
+        const int n = scnt[axis][i];
         if (n == w) continue;
         if (n < K) {
           solved = false;
           continue;
         }
         Op op{axis, i, {}};
+        const int oaxis = 1 - axis;
         for (int j = 0; j < w; j++) {
           if (Ps[cell(axis, i, j)]) continue;
-          const int oaxis = 1 - axis;
-          if (count(Ps, oaxis, j, i) == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
+          // orthogonal axis j is completed by this operation iff (i, j) is its only missing cell
+          if (scnt[oaxis][j] == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
         }
-        for (int j = 0; j < w; j++) Ps[cell(axis, i, j)] = 1;
+        for (int j = 0; j < w; j++) {
+          uint8_t& v = Ps[cell(axis, i, j)];
+          if (!v) {
+            v = 1;
+            scnt[oaxis][j]++;
+          }
+        }
+        scnt[axis][i] = w;
         ops.push_back(std::move(op));
         progress = true;
       }
@@ -972,12 +989,20 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
       return CDA_OK;
     };
     auto apply = [&](size_t q) {
-      for (int j = 0; j < w; j++) P[cell(ops[q].axis, ops[q].idx, j)] = 1;
+      const int axis = ops[q].axis, idx = ops[q].idx;
+      for (int j = 0; j < w; j++) {
+        uint8_t& v = P[cell(axis, idx, j)];
+        if (!v) {
+          v = 1;
+          pcnt[1 - axis][j]++;
+        }
+      }
+      pcnt[axis][idx] = w;
     };
     size_t b0 = 0;
     while (b0 < ops.size()) {
       size_t b1 = b0;
-      while (b1 < ops.size() && b1 - b0 < trees_cap / 2 && count(P, ops[b1].axis, ops[b1].idx, -1) >= K) b1++;
+      while (b1 < ops.size() && b1 - b0 < trees_cap / 2 && pcnt[ops[b1].axis][ops[b1].idx] >= K) b1++;
       if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
       int bad = 0;
       rc = run_ops(b0, b1, &bad);
