@@ -21,6 +21,7 @@
 //    in LDS, radix-2 layers, constant matrix applied with v_bitop3 masks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <vector>
 
@@ -889,9 +890,16 @@ int launch_rs_encode16(const RsJob& j, hipStream_t s) {
   a.m = 1 << a.log2m;
   a.cw_per_blk = j.cw_per_blk;
   const int units = j.shard_len / 64;
-  // LDS budget 128 KiB: m * 64 B per unit column
+  // LDS per workgroup: m * 64 B per unit column.  The budget sets the occupancy (LDS-bound: 160 KiB per CU)
+  // against how many layers have wave-uniform constants (D * U >= 64).  Measured at k = 512 (m = 512):
+  // 32 KiB (U = 1, 5 workgroups per CU) rows 0.47 + cols 0.83 ms per 2 squares, 64 KiB (U = 2) 0.56 + 1.03,
+  // 128 KiB 0.83 + 1.55 -- occupancy wins over the extra lane-masked layers.
+  static const size_t budget = [] {
+    const char* e = getenv("CDA_RS16_LDS_KB");
+    return (size_t)(e ? atoi(e) : 32) * 1024;
+  }();
   int U = 8;
-  while (U > 1 && ((size_t)a.m * 64 * U > 64 * 1024 || units % U)) U >>= 1;
+  while (U > 1 && ((size_t)a.m * 64 * U > budget || units % U)) U >>= 1;
   if ((size_t)a.m * 64 * U > 128 * 1024) return -2;  // m > 2048: not on the device path yet
   a.U = U;
   a.log2U = ilog2(U);
