@@ -149,6 +149,16 @@ def extend_commit_split(ops, k, ods_rows, group=None):
     (CDA_E_NS_ORDER with axis / index / leaf) like cda_extend_commit.
     """
     import torch
+    if ops.device.type == "cuda":
+        # every torch op and collective of the split on ops.stream, the stream the libcda calls use (a
+        # collective orders itself after the CURRENT stream only; ADVICE r01)
+        with torch.cuda.stream(ops.stream):
+            return _extend_commit_split(ops, k, ods_rows, group)
+    return _extend_commit_split(ops, k, ods_rows, group)
+
+
+def _extend_commit_split(ops, k, ods_rows, group):
+    import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
