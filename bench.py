@@ -294,7 +294,7 @@ def square_measure(ctx, reps=3):
     from cda import square as S
     rng = np.random.default_rng(3)
     txs = []
-    for i in range(128):
+    for i in range(120):
         ns_id = bytes(18) + bytes([1 + i % 255]) + bytes(rng.integers(0, 256, 9, dtype=np.uint8))
         data = bytes(rng.integers(0, 256, 60 * 1024, dtype=np.uint8))
         blob = b"\x0a" + S.varint(len(ns_id)) + ns_id + b"\x12" + S.varint(len(data)) + data
