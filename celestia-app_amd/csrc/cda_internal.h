@@ -80,6 +80,15 @@ int launch_axes_roots(const uint8_t* d_eds, int k, const int* d_axes, int axis0,
 int launch_nmt_fold(void* d_nodes, void* d_scratch, void* d_roots, int ntrees, int log2n, hipStream_t s);
 int launch_parity_compare(const uint8_t* d_eds, int k, const int* d_axes, int naxes, const uint8_t* d_par,
                           unsigned* d_flags, hipStream_t s);
+// repair verification fused: leaves, levels and root check of ntrees axis trees (one workgroup each);
+// failing tree t: *d_flag = min(*d_flag, base + t), or d_flag[t] = 1 when per_tree
+int launch_axes_verify(const uint8_t* d_eds, int k, const int* d_axes, int ntrees, const uint8_t* d_want_rows,
+                       const uint8_t* d_want_cols, unsigned* d_flag, unsigned base, bool per_tree, hipStream_t s);
+// *d_flag = min(*d_flag, base + t) for every tree t whose status is dirty or whose root differs from
+// want_{rows,cols}[index] (repair's root verification without a host round trip)
+int launch_roots_check(const void* d_recs, const unsigned long long* d_status, const int* d_axes, int n,
+                       const uint8_t* d_want_rows, const uint8_t* d_want_cols, unsigned* d_flag, unsigned base,
+                       hipStream_t s);
 
 // Blob of a share-commitment batch (go-square inclusion.CreateCommitment), built by the host.
 struct BlobDesc {

@@ -26,6 +26,10 @@ struct cda_ctx {
   int chunk_blocks = 0;
   // CDA_FUSED=1: extension fused with leaf hashing (measured no faster; see rs_kernels.hip)
   bool fused = false;
+  // CDA_REPAIR_OVERLAP=0: repair verifies each batch on the decode stream instead of a second stream
+  bool repair_overlap = true;
+  // CDA_REPAIR_FUSED=0: verify with the generic leaf + per-level launches instead of one fused launch
+  bool repair_fused_verify = true;
   hipStream_t sub[kMaxSub] = {};
   // Workspace ordering across streams: the device-resident entry points enqueue on the caller's
   // stream but use this ctx's workspace (leaf/scratch records).  ws_event marks the end of the
@@ -44,7 +48,9 @@ struct cda_ctx {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf ods, eds, leaf, scratch, roots, dah, status, host_status, plan, payload;
+  Buf ods, eds, leaf, scratch, roots, dah, status, plan, payload;
+  // repair: device root table + per-sweep descriptors, and their pinned host staging
+  Buf rdesc, rstage;
   // profiling
   bool prof = false;
   struct Pending {

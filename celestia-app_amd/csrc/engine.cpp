@@ -21,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ctx.h"
@@ -71,6 +72,17 @@ int ensure(cda_ctx* c, cda_ctx::Buf& b, size_t bytes) {
   b.p = nullptr;
   b.cap = 0;
   if (!dev_ok(c, hipMalloc(&b.p, bytes ? bytes : 16), "hipMalloc")) return CDA_E_DEVICE;
+  b.cap = bytes;
+  return CDA_OK;
+}
+
+// pinned host buffer (hipHostMalloc), grown like ensure()
+static int ensure_host(cda_ctx* c, cda_ctx::Buf& b, size_t bytes) {
+  if (b.cap >= bytes) return CDA_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  if (!dev_ok(c, hipHostMalloc(&b.p, bytes ? bytes : 16, hipHostMallocDefault), "hipHostMalloc")) return CDA_E_DEVICE;
   b.cap = bytes;
   return CDA_OK;
 }
@@ -330,6 +342,8 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_PIPELINE")) c->pipe_chunks = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("CDA_CHUNK")) c->chunk_blocks = std::max(0, atoi(e));
   if (const char* e = getenv("CDA_FUSED")) c->fused = atoi(e) != 0;
+  if (const char* e = getenv("CDA_REPAIR_OVERLAP")) c->repair_overlap = atoi(e) != 0;
+  if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;
@@ -350,9 +364,10 @@ void cda_free(cda_ctx* c) {
     Lock l(c);
     (void)hipStreamSynchronize(c->stream);
     flush_profile(c);
-    for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status, &c->plan, &c->payload})
+    for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status, &c->plan, &c->payload,
+                    &c->rdesc})
       if (b->p) (void)hipFree(b->p);
-    if (c->host_status.p) (void)hipHostFree(c->host_status.p);
+    if (c->rstage.p) (void)hipHostFree(c->rstage.p);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < cda_ctx::kMaxSub; i++) {
       if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
@@ -747,15 +762,84 @@ int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uin
 //     axis with >= k shares is decoded, its root and the roots of orthogonal
 //     axes it completes are verified, then its cells are inserted; a sweep
 //     without progress is ErrUnrepairableDataSquare.
-// The host replays exactly that order on the presence bitmap (control only) and
-// runs every decode / root / re-encode on the GPU, batching consecutive
-// operations that are already decodable at the batch start; a batch with a
-// failing root check is replayed one operation at a time (see below), so a
-// Byzantine report and the square left "most repaired prior to the Byzantine
-// axis" are exactly the sequential reference's.
+// The host replays exactly that order on presence bitsets (control only), for
+// every sweep up front as if all checks pass, and the GPU runs every decode /
+// root / re-encode: consecutive operations already decodable at the batch start
+// form a batch, all batches are enqueued at once (decodes in order on one
+// stream, each batch's root check on another), and the host waits once.  The
+// first batch with a failing root check is replayed one operation at a time
+// (see below), so a Byzantine report and the square left "most repaired prior
+// to the Byzantine axis" are exactly the sequential reference's.
+extern "C++" {
 namespace {
 inline int enc_axis(int axis, int idx) { return (axis << 24) | idx; }
-}
+
+// Presence of the w x w cells as row and column bitsets with per-axis counts: a crossword step
+// costs O(w / 64 + cells it fills) on the host instead of O(w) byte scans.
+struct Presence {
+  int w = 0, words = 0;
+  uint64_t full = 0;              // valid bits of each word (w < 64: one partial word)
+  std::vector<uint64_t> bits[2];  // [axis][idx * words + j / 64] bit j % 64 = cell j of axis idx present
+  std::vector<int> cnt[2];        // present cells per axis
+  void init(int w_, const uint8_t* p) {
+    w = w_;
+    words = (w + 63) / 64;
+    full = w >= 64 ? ~0ull : ((1ull << w) - 1);
+    for (int a = 0; a < 2; a++) {
+      bits[a].assign((size_t)w * words, 0);
+      cnt[a].assign(w, 0);
+    }
+    for (int r = 0; r < w; r++)
+      for (int q = 0; q < w; q++)
+        if (p[(size_t)r * w + q]) {
+          bits[CDA_AXIS_ROW][(size_t)r * words + (q >> 6)] |= 1ull << (q & 63);
+          bits[CDA_AXIS_COL][(size_t)q * words + (r >> 6)] |= 1ull << (r & 63);
+          cnt[CDA_AXIS_ROW][r]++;
+          cnt[CDA_AXIS_COL][q]++;
+        }
+  }
+  // f(j) for every missing cell j of axis (a, idx), j ascending
+  template <class F>
+  void missing(int a, int idx, F f) const {
+    const uint64_t* b = bits[a].data() + (size_t)idx * words;
+    for (int wd = 0; wd < words; wd++)
+      for (uint64_t m = ~b[wd] & full; m; m &= m - 1) f(wd * 64 + __builtin_ctzll(m));
+  }
+  // mark every cell of axis (a, idx) present
+  void fill(int a, int idx) {
+    const int o = 1 - a;
+    missing(a, idx, [&](int j) {
+      bits[o][(size_t)j * words + (idx >> 6)] |= 1ull << (idx & 63);
+      cnt[o][j]++;
+    });
+    uint64_t* b = bits[a].data() + (size_t)idx * words;
+    for (int wd = 0; wd < words; wd++) b[wd] = full;
+    cnt[a][idx] = w;
+  }
+  // presence of axis (a, idx)'s cells, one byte (0/1) each
+  void bytes(int a, int idx, uint8_t* out) const {
+    static const struct Expand {
+      uint64_t t[256];
+      Expand() {
+        for (int v = 0; v < 256; v++) {
+          t[v] = 0;
+          for (int i = 0; i < 8; i++) t[v] |= (uint64_t)((v >> i) & 1) << (8 * i);
+        }
+      }
+    } ex;
+    const uint64_t* b = bits[a].data() + (size_t)idx * words;
+    if (w < 8) {
+      for (int j = 0; j < w; j++) out[j] = (b[0] >> j) & 1;
+      return;
+    }
+    for (int j = 0; j < w; j += 8) {
+      const uint64_t v = ex.t[(b[j >> 6] >> (j & 63)) & 0xFF];
+      memcpy(out + j, &v, 8);
+    }
+  }
+};
+}  // namespace
+}  // extern "C++"
 
 int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, cda_err_info* err) {
@@ -768,29 +852,141 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
   const size_t ncell = (size_t)w * w, eds_b = ncell * CDA_SHARE;
   hipStream_t s = c->stream;
   int rc;
-  // workspace: eds | parity scratch (2 * w * k shards) | roots/nodes/scratch for up to 2w trees
-  const size_t trees_cap = (size_t)2 * w;
+  // Generic verification workspace (sequential replay, CDA_REPAIR_FUSED=0): leaf / level records
+  // for up to 4w trees.  Repair descriptors (device, staged in pinned host memory at the same
+  // offsets): an operation completes an axis, so a repair has at most 2w operations, 4w verified
+  // axes (each axis is its own operation's and at most one other operation's orthogonal
+  // completion) and 2w batches.
+  //   off[2w] | stride[2w] | pres[2w][w] | vaxes[4w] | sanity axes[2w] | all axes[2w]
+  //   | batch flags[2w] | sanity root flags[2w] | parity flags[2w]      (after the 2w x 90 B roots)
+  const size_t trees_cap = (size_t)4 * w, W = (size_t)w;
+  const size_t want_b = (2 * W * CDA_NODE_SIZE + 255) & ~(size_t)255;
+  const size_t o_off = 0, o_str = o_off + 2 * W * 8, o_pres = o_str + 2 * W * 8, o_ax = o_pres + 2 * W * W,
+               o_sax = o_ax + 4 * W * 4, o_all = o_sax + 2 * W * 4, o_bfl = o_all + 2 * W * 4,
+               o_sfl = o_bfl + 2 * W * 4, o_pfl = o_sfl + 2 * W * 4, desc_b = o_pfl + 2 * W * 4;
   if ((rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->ods, eds_b)) ||
       (rc = ensure(c, c->leaf, trees_cap * w * CDA_REC_BYTES)) ||
       (rc = ensure(c, c->scratch, trees_cap * w * CDA_REC_BYTES)) ||
       (rc = ensure(c, c->roots, trees_cap * CDA_REC_BYTES)) || (rc = ensure(c, c->status, trees_cap * 8 + 64)) ||
-      (rc = ensure(c, c->dah, trees_cap * (16 + 2 * (size_t)w) + trees_cap * 4 + 64)))
+      (rc = ensure(c, c->dah, trees_cap * (16 + W) + 64)) || (rc = ensure(c, c->rdesc, want_b + desc_b)) ||
+      (rc = ensure_host(c, c->rstage, desc_b)))
     return rc;
   uint8_t* d_eds = (uint8_t*)c->eds.p;
   uint8_t* d_par = (uint8_t*)c->ods.p;
-  if (!dev_ok(c, hipMemcpyAsync(d_eds, eds, eds_b, hipMemcpyHostToDevice, s), "H2D")) return CDA_E_DEVICE;
-  std::vector<uint8_t> P(present, present + ncell);
-  for (auto& v : P) v = v ? 1 : 0;
-  auto cell = [&](int axis, int idx, int i) -> size_t {
-    return axis == CDA_AXIS_ROW ? (size_t)idx * w + i : (size_t)i * w + idx;
-  };
-  auto count = [&](const std::vector<uint8_t>& p, int axis, int idx, int skip) {
-    int n = 0;
-    for (int i = 0; i < w; i++) n += (i != skip && p[cell(axis, idx, i)]) ? 1 : 0;
-    return n;
-  };
+  const uint8_t* d_want = (const uint8_t*)c->rdesc.p;
+  uint8_t* h = (uint8_t*)c->rstage.p;
+  uint8_t* dd = (uint8_t*)c->rdesc.p + want_b;
+  unsigned* d_bfl = (unsigned*)(dd + o_bfl);
+  const unsigned* bfl = (const unsigned*)(h + o_bfl);
+  const unsigned* sfl = (const unsigned*)(h + o_sfl);
+  const unsigned* pfl = (const unsigned*)(h + o_pfl);
+  // The EDS upload (pageable memory: the copy occupies the calling thread) runs on a helper thread
+  // while this one plans the whole repair on the presence bitsets.
+  bool h2d_ok = false;
+  std::thread h2d([&] {
+    (void)hipSetDevice(c->device);
+    h2d_ok = hipMemcpyAsync(d_eds, eds, eds_b, hipMemcpyHostToDevice, s) == hipSuccess;
+  });
+  Presence P;
+  P.init(w, present);
   const uint8_t* want[2] = {row_roots, col_roots};
-  // GPU roots of a list of axes -> host records
+
+  // ---- plan: prerepairSanityCheck axes, then every crossword sweep on the optimistic presence ----
+  std::vector<int> sane;  // complete axes: i ascending, row before column
+  for (int i = 0; i < w; i++) {
+    if (P.cnt[CDA_AXIS_ROW][i] == w) sane.push_back(enc_axis(CDA_AXIS_ROW, i));
+    if (P.cnt[CDA_AXIS_COL][i] == w) sane.push_back(enc_axis(CDA_AXIS_COL, i));
+  }
+  struct Op {
+    int axis, idx;
+    std::vector<int> ortho;
+  };
+  struct Batch {
+    size_t q0, q1, v0, v1;  // operations [q0, q1), their verified axes vall[v0, v1)
+  };
+  std::vector<Op> ops;
+  std::vector<Batch> bat;
+  std::vector<int> vall;
+  bool solved = false;
+  {
+    Presence Pq = P;
+    for (;;) {
+      // replay one sweep: row i, then column i, for i = 0..w-1
+      Presence Ps = Pq;
+      const size_t first = ops.size();
+      bool sweep_solved = true;
+      for (int i = 0; i < w; i++) {
+        for (int axis = 0; axis < 2; axis++) {
+          const int n = Ps.cnt[axis][i];
+          if (n == w) continue;
+          if (n < K) {
+            sweep_solved = false;
+            continue;
+          }
+          Op op{axis, i, {}};
+          const int oaxis = 1 - axis;
+          // orthogonal axis j is completed by this operation iff (i, j) is its only missing cell
+          Ps.missing(axis, i, [&](int j) {
+            if (Ps.cnt[oaxis][j] == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
+          });
+          Ps.fill(axis, i);
+          ops.push_back(std::move(op));
+        }
+      }
+      if (ops.size() > 2 * W) return CDA_E_ARG;  // cannot happen: each operation completes an axis
+      // batches of operations already decodable at the batch start
+      for (size_t b0 = first; b0 < ops.size();) {
+        size_t b1 = b0;
+        while (b1 < ops.size() && Pq.cnt[ops[b1].axis][ops[b1].idx] >= K) b1++;
+        if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
+        Batch bt{b0, b1, vall.size(), 0};
+        for (size_t q = b0; q < b1; q++) {
+          const Op& op = ops[q];
+          ((long long*)(h + o_off))[q] =
+              op.axis == CDA_AXIS_ROW ? (long long)op.idx * w * CDA_SHARE : (long long)op.idx * CDA_SHARE;
+          ((long long*)(h + o_str))[q] = op.axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
+          Pq.bytes(op.axis, op.idx, h + o_pres + q * W);  // the presence at the batch start
+          vall.push_back(enc_axis(op.axis, op.idx));      // own axis, then orthogonal axes, in order
+          for (int o : op.ortho) vall.push_back(o);
+        }
+        bt.v1 = vall.size();
+        bat.push_back(bt);
+        for (size_t q = b0; q < b1; q++) Pq.fill(ops[q].axis, ops[q].idx);
+        b0 = b1;
+      }
+      if (sweep_solved) {
+        solved = true;
+        break;
+      }
+      if (ops.size() == first) break;  // no progress: unrepairable once every batch has passed
+    }
+  }
+  if (vall.size() > 4 * W) return CDA_E_ARG;  // cannot happen: the bound above
+  const size_t nbat = bat.size();
+  memcpy(h + o_ax, vall.data(), vall.size() * 4);
+  memcpy(h + o_sax, sane.data(), sane.size() * 4);
+  for (int i = 0; i < w; i++) {
+    ((int*)(h + o_all))[i] = enc_axis(CDA_AXIS_ROW, i);
+    ((int*)(h + o_all))[w + i] = enc_axis(CDA_AXIS_COL, i);
+  }
+  h2d.join();
+  if (!h2d_ok) {
+    c->last_err = "H2D failed";
+    return CDA_E_DEVICE;
+  }
+  const int* d_ax = (const int*)(dd + o_ax);
+  const int* d_sax = (const int*)(dd + o_sax);
+  const int* d_all = (const int*)(dd + o_all);
+  if (!dev_ok(c, hipMemcpyAsync(c->rdesc.p, row_roots, W * CDA_NODE_SIZE, hipMemcpyHostToDevice, s), "H2D") ||
+      !dev_ok(c, hipMemcpyAsync((uint8_t*)c->rdesc.p + W * CDA_NODE_SIZE, col_roots, W * CDA_NODE_SIZE,
+                                hipMemcpyHostToDevice, s),
+              "H2D") ||
+      !dev_ok(c, hipMemcpyAsync(dd, h, o_bfl, hipMemcpyHostToDevice, s), "H2D") ||
+      !dev_ok(c, hipMemsetAsync(d_bfl, 0xFF, 2 * W * 4, s), "memset") ||
+      !dev_ok(c, hipMemsetAsync(dd + o_sfl, 0, 4 * W * 4, s), "memset"))
+    return CDA_E_DEVICE;
+
+  // GPU roots of a list of axes -> host records (sequential replay and the generic sanity path)
   std::vector<uint8_t> recs;
   std::vector<uint64_t> st;
   auto roots_of = [&](const std::vector<int>& axes) -> int {
@@ -820,210 +1016,174 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
     return memcmp(recs.data() + t * CDA_REC_BYTES, want[axis] + (size_t)idx * CDA_NODE_SIZE, CDA_NODE_SIZE) == 0;
   };
   auto finish = [&](int code, int axis, int idx) -> int {
-    if (!dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H") ||
-        !dev_ok(c, hipStreamSynchronize(s), "sync"))
-      return CDA_E_DEVICE;
+    if (!dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H")) return CDA_E_DEVICE;
+    for (int r = 0; r < w; r++) P.bytes(CDA_AXIS_ROW, r, present + (size_t)r * w);
+    if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
     flush_profile(c);
-    memcpy(present, P.data(), ncell);
     if (code != CDA_OK) set_err(err, code, axis, idx, -1, -1);
     return code;
   };
+  // Verification streams.  Decodes run in order on `s`; batch b's verification runs after decode b
+  // on a second stream, overlapping decode b+1 (which writes only cells missing after batch b, and
+  // every axis batch b verifies is complete after it).  The fused kernel keeps its trees in LDS, so
+  // batches verify concurrently on 3 streams; the generic path shares the leaf / level workspace.
+  const int nvs = c->repair_overlap ? (c->repair_fused_verify ? 3 : 1) : 0;
+  auto vstream = [&](size_t b) { return nvs ? c->sub[cda_ctx::kMaxSub - 1 - (int)(b % nvs)] : s; };
+  auto fork = [&](hipStream_t v) {
+    return v == s || (dev_ok(c, hipEventRecord(c->fork_ev, s), "event") &&
+                      dev_ok(c, hipStreamWaitEvent(v, c->fork_ev, 0), "wait"));
+  };
+  auto join = [&]() {
+    for (int i = 0; i < nvs; i++)
+      if (!dev_ok(c, hipEventRecord(c->join_ev[i], c->sub[cda_ctx::kMaxSub - 1 - i]), "event") ||
+          !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[i], 0), "wait"))
+        return false;
+    return true;
+  };
 
-  // ---- prerepairSanityCheck ----
-  {
-    std::vector<int> axes;
-    std::vector<uint8_t> rowc(w), colc(w);
-    for (int i = 0; i < w; i++) {
-      rowc[i] = count(P, CDA_AXIS_ROW, i, -1) == w;
-      colc[i] = count(P, CDA_AXIS_COL, i, -1) == w;
-      if (rowc[i]) axes.push_back(enc_axis(CDA_AXIS_ROW, i));
-      if (colc[i]) axes.push_back(enc_axis(CDA_AXIS_COL, i));
+  // ---- prerepairSanityCheck, enqueued: every complete row / column must match its root and
+  // re-encode to its own parity.  Crossword decodes write only missing cells, never a cell of a
+  // complete axis, so the check runs concurrently with them; it is evaluated first afterwards. ----
+  std::vector<uint8_t> san_bad(sane.size(), 0);
+  if (!sane.empty()) {
+    if (!c->repair_fused_verify) {  // generic: roots through the workspace, compared on the host
+      if ((rc = roots_of(sane))) return rc;
+      for (size_t t = 0; t < sane.size(); t++) san_bad[t] = root_ok(t, sane[t]) ? 0 : 1;
     }
-    std::vector<unsigned> pflag_row(w, 0), pflag_col(w, 0);
-    if (!axes.empty()) {
-      if ((rc = roots_of(axes))) return rc;
-      // re-encode every row and column data half; compare the complete ones
-      unsigned* d_flags = (unsigned*)((uint8_t*)c->dah.p + trees_cap * (16 + 2 * (size_t)w));
-      int* d_axes = (int*)c->dah.p;
-      std::vector<int> all(2 * w);
-      for (int i = 0; i < w; i++) {
-        all[i] = enc_axis(CDA_AXIS_ROW, i);
-        all[w + i] = enc_axis(CDA_AXIS_COL, i);
-      }
-      if (!dev_ok(c, hipMemcpyAsync(d_axes, all.data(), all.size() * 4, hipMemcpyHostToDevice, s), "H2D") ||
-          !dev_ok(c, hipMemsetAsync(d_flags, 0, 2 * w * 4, s), "memset"))
+    hipStream_t v = vstream(0);
+    if (!fork(v)) return CDA_E_DEVICE;
+    if (c->repair_fused_verify) {
+      ProfScope ps(c, "repair_roots", v);
+      if (launch_axes_verify(d_eds, K, d_sax, (int)sane.size(), d_want, d_want + W * CDA_NODE_SIZE,
+                             (unsigned*)(dd + o_sfl), 0, true, v))
         return CDA_E_DEVICE;
-      for (int axis = 0; axis < 2; axis++) {
-        RsJob j{};
-        j.src = d_eds;
-        j.src_cw = axis == CDA_AXIS_ROW ? (long long)w * CDA_SHARE : CDA_SHARE;
-        j.src_sh = axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
-        j.dst = d_par + (size_t)axis * w * K * CDA_SHARE;
-        j.dst_cw = (long long)K * CDA_SHARE;
-        j.dst_sh = CDA_SHARE;
-        j.k = K;
-        j.cw_per_blk = w;
-        j.nblk = 1;
-        j.shard_len = CDA_SHARE;
-        ProfScope ps(c, "repair_reencode", s);
-        const int lr = 2 * K <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
-        if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
-        if (launch_parity_compare(d_eds, K, d_axes + axis * w, w, j.dst, d_flags + axis * w, s)) return CDA_E_DEVICE;
-      }
-      std::vector<unsigned> fl(2 * w);
-      if (!dev_ok(c, hipMemcpyAsync(fl.data(), d_flags, 2 * w * 4, hipMemcpyDeviceToHost, s), "D2H") ||
-          !dev_ok(c, hipStreamSynchronize(s), "sync"))
+    }
+    for (int axis = 0; axis < 2; axis++) {  // re-encode every row and column data half
+      RsJob j{};
+      j.src = d_eds;
+      j.src_cw = axis == CDA_AXIS_ROW ? (long long)w * CDA_SHARE : CDA_SHARE;
+      j.src_sh = axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
+      j.dst = d_par + (size_t)axis * w * K * CDA_SHARE;
+      j.dst_cw = (long long)K * CDA_SHARE;
+      j.dst_sh = CDA_SHARE;
+      j.k = K;
+      j.cw_per_blk = w;
+      j.nblk = 1;
+      j.shard_len = CDA_SHARE;
+      ProfScope ps(c, "repair_reencode", v);
+      const int lr = 2 * K <= 256 ? launch_rs_encode8(j, v) : launch_rs_encode16(j, v);
+      if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+      if (launch_parity_compare(d_eds, K, d_all + axis * w, w, j.dst, (unsigned*)(dd + o_pfl) + axis * w, v))
         return CDA_E_DEVICE;
-      for (int i = 0; i < w; i++) {
-        pflag_row[i] = fl[i];
-        pflag_col[i] = fl[w + i];
-      }
-      // report in a fixed order: i ascending; row root, col root, row parity, col parity
-      size_t t = 0;
-      std::vector<int> rok(w, 1), cok(w, 1);
-      for (int i = 0; i < w; i++) {
-        if (rowc[i]) rok[i] = root_ok(t++, enc_axis(CDA_AXIS_ROW, i));
-        if (colc[i]) cok[i] = root_ok(t++, enc_axis(CDA_AXIS_COL, i));
-      }
-      for (int i = 0; i < w; i++) {
-        if (rowc[i] && !rok[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_ROW, i);
-        if (colc[i] && !cok[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_COL, i);
-        if (rowc[i] && pflag_row[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_ROW, i);
-        if (colc[i] && pflag_col[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_COL, i);
-      }
     }
   }
 
-  // ---- solveCrossword ----
-  struct Op {
-    int axis, idx;
-    std::vector<int> ortho;
-  };
-  long long* d_off = (long long*)c->dah.p;
-  long long* d_stride = d_off + trees_cap;
-  uint8_t* d_pres = (uint8_t*)(d_stride + trees_cap);
-  // present-cell counts per row / column of P, kept in step with it (the replay below is O(w^2) per sweep)
-  std::vector<int> pcnt[2] = {std::vector<int>(w, 0), std::vector<int>(w, 0)};
-  for (int r = 0; r < w; r++)
-    for (int q = 0; q < w; q++)
-      if (P[(size_t)r * w + q]) {
-        pcnt[CDA_AXIS_ROW][r]++;
-        pcnt[CDA_AXIS_COL][q]++;
+  // ---- solveCrossword, optimistic: every batch as if all checks pass, one wait at the end ----
+  // A batch whose every root check passes equals the sequential rsmt2d run: each checked axis then
+  // holds its committed values, so every decode saw only true shares and the sequential decode
+  // (with more shares) gives the same bytes.  Presence only grows and a decode writes only cells
+  // missing in its own presence, so work enqueued after a failing batch never writes a cell that
+  // batch (or an earlier one) reads: the device state at the first failing batch's start is
+  // intact, and that batch is replayed one operation at a time with the presence each operation
+  // sees in rsmt2d's order, so Byzantine reports (axis, index, the square repaired so far) are
+  // exactly the sequential ones even when a row and a column of a batch write the same cell.
+  auto enqueue_batches = [&](size_t from) -> int {
+    for (size_t b = from; b < nbat; b++) {
+      const Batch& bt = bat[b];
+      {
+        ProfScope ps(c, "repair_decode", s);
+        const int lr = launch_rs_decode(d_eds, (const long long*)(dd + o_off) + bt.q0,
+                                        (const long long*)(dd + o_str) + bt.q0, dd + o_pres + bt.q0 * W,
+                                        (int)(bt.q1 - bt.q0), K, CDA_SHARE, s);
+        if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
       }
-  for (;;) {
-    // replay one sweep on the presence bitmap
-    std::vector<uint8_t> Ps = P;
-    std::vector<int> scnt[2] = {pcnt[0], pcnt[1]};
-    std::vector<Op> ops;
-    bool solved = true, progress = false;
-    for (int i = 0; i < w; i++) {
-      for (int axis = 0; axis < 2; axis++) {
-        const int n = scnt[axis][i];
-        if (n == w) continue;
-        if (n < K) {
-          solved = false;
-          continue;
-        }
-        Op op{axis, i, {}};
-        const int oaxis = 1 - axis;
-        for (int j = 0; j < w; j++) {
-          if (Ps[cell(axis, i, j)]) continue;
-          // orthogonal axis j is completed by this operation iff (i, j) is its only missing cell
-          if (scnt[oaxis][j] == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
-        }
-        for (int j = 0; j < w; j++) {
-          uint8_t& v = Ps[cell(axis, i, j)];
-          if (!v) {
-            v = 1;
-            scnt[oaxis][j]++;
-          }
-        }
-        scnt[axis][i] = w;
-        ops.push_back(std::move(op));
-        progress = true;
+      hipStream_t v = vstream(b);
+      if (!fork(v)) return CDA_E_DEVICE;
+      const size_t nv = bt.v1 - bt.v0;
+      if (c->repair_fused_verify) {
+        ProfScope ps(c, "repair_roots", v);
+        if (launch_axes_verify(d_eds, K, d_ax + bt.v0, (int)nv, d_want, d_want + W * CDA_NODE_SIZE, d_bfl + b, 0,
+                               false, v))
+          return CDA_E_DEVICE;
+        continue;
+      }
+      for (size_t v0 = 0; v0 < nv; v0 += trees_cap) {  // chunks of at most trees_cap trees
+        const int n = (int)std::min(trees_cap, nv - v0);
+        if (!dev_ok(c, hipMemsetAsync(c->status.p, 0xFF, (size_t)n * 8, v), "memset")) return CDA_E_DEVICE;
+        ProfScope ps(c, "repair_roots", v);
+        if (launch_axes_roots(d_eds, K, d_ax + bt.v0 + v0, 0, n, 0, w, c->leaf.p, c->scratch.p, c->roots.p,
+                              (unsigned long long*)c->status.p, v) ||
+            launch_roots_check(c->roots.p, (const unsigned long long*)c->status.p, d_ax + bt.v0 + v0, n, d_want,
+                               d_want + W * CDA_NODE_SIZE, d_bfl + b, (unsigned)v0, v))
+          return CDA_E_DEVICE;
       }
     }
-    // Execute in batches of operations already decodable at the batch start.  A batch whose every
-    // root check passes equals the sequential rsmt2d run: each checked axis then holds its committed
-    // values, so every decode saw only true shares and the sequential decode (with more shares) gives
-    // the same bytes.  A batch with any failing check is replayed one operation at a time with the
-    // presence that operation sees in rsmt2d's order, so Byzantine reports (axis, index, the square
-    // repaired so far) are exactly the sequential ones even when a row and a column of the batch
-    // write the same cell.
-    // run_ops: decode ops [b0, b1) with the presence P, verify own + orthogonal roots in order.
-    // Returns CDA_OK, CDA_E_BYZANTINE (*bad = failing axis code) or an error; P is not modified.
-    auto run_ops = [&](size_t b0, size_t b1, int* bad) -> int {
-      const int nb = (int)(b1 - b0);
-      std::vector<long long> off(nb), stride(nb);
-      std::vector<uint8_t> pres((size_t)nb * w);
-      for (int q = 0; q < nb; q++) {
-        const Op& op = ops[b0 + q];
-        off[q] = op.axis == CDA_AXIS_ROW ? (long long)op.idx * w * CDA_SHARE : (long long)op.idx * CDA_SHARE;
-        stride[q] = op.axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
-        for (int j = 0; j < w; j++) pres[(size_t)q * w + j] = P[cell(op.axis, op.idx, j)];
-      }
-      if (!dev_ok(c, hipMemcpyAsync(d_off, off.data(), nb * 8, hipMemcpyHostToDevice, s), "H2D") ||
-          !dev_ok(c, hipMemcpyAsync(d_stride, stride.data(), nb * 8, hipMemcpyHostToDevice, s), "H2D") ||
-          !dev_ok(c, hipMemcpyAsync(d_pres, pres.data(), pres.size(), hipMemcpyHostToDevice, s), "H2D"))
+    if (!join() ||
+        !dev_ok(c, hipMemcpyAsync(h + o_bfl, dd + o_bfl, o_pfl + 2 * W * 4 - o_bfl, hipMemcpyDeviceToHost, s),
+                "D2H") ||
+        !dev_ok(c, hipStreamSynchronize(s), "sync"))
+      return CDA_E_DEVICE;
+    return CDA_OK;
+  };
+  if ((rc = enqueue_batches(0))) return rc;
+
+  // sanity report in a fixed order: i ascending; row root, col root, row parity, col parity
+  if (!sane.empty()) {
+    std::vector<uint8_t> rbad(w, 0), cbad(w, 0);
+    for (size_t t = 0; t < sane.size(); t++) {
+      const bool bad = c->repair_fused_verify ? sfl[t] != 0 : san_bad[t] != 0;
+      (sane[t] >> 24 == CDA_AXIS_ROW ? rbad : cbad)[sane[t] & 0xFFFFFF] = bad;
+    }
+    for (int i = 0; i < w; i++) {
+      const bool rowc = P.cnt[CDA_AXIS_ROW][i] == w, colc = P.cnt[CDA_AXIS_COL][i] == w;
+      if (rowc && rbad[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_ROW, i);
+      if (colc && cbad[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_COL, i);
+      if (rowc && pfl[i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_ROW, i);
+      if (colc && pfl[w + i]) return finish(CDA_E_BYZANTINE, CDA_AXIS_COL, i);
+    }
+  }
+  for (size_t b = 0; b < nbat;) {
+    if (bfl[b] == ~0u) {
+      for (size_t q = bat[b].q0; q < bat[b].q1; q++) P.fill(ops[q].axis, ops[q].idx);
+      b++;
+      continue;
+    }
+    if (bat[b].q1 - bat[b].q0 == 1) {
+      const int bad = vall[bat[b].v0 + bfl[b]];
+      return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
+    }
+    for (size_t q = bat[b].q0; q < bat[b].q1; q++) {  // sequential replay of the failed batch
+      // decode op q with the presence it sees in order, then verify its own and orthogonal roots
+      long long off = ((const long long*)(h + o_off))[q], stride = ((const long long*)(h + o_str))[q];
+      std::vector<uint8_t> pres(W);
+      P.bytes(ops[q].axis, ops[q].idx, pres.data());
+      long long* d_off = (long long*)c->dah.p;
+      uint8_t* d_pres = (uint8_t*)(d_off + 2);
+      if (!dev_ok(c, hipMemcpyAsync(d_off, &off, 8, hipMemcpyHostToDevice, s), "H2D") ||
+          !dev_ok(c, hipMemcpyAsync(d_off + 1, &stride, 8, hipMemcpyHostToDevice, s), "H2D") ||
+          !dev_ok(c, hipMemcpyAsync(d_pres, pres.data(), W, hipMemcpyHostToDevice, s), "H2D"))
         return CDA_E_DEVICE;
       {
         ProfScope ps(c, "repair_decode", s);
-        const int lr = launch_rs_decode(d_eds, d_off, d_stride, d_pres, nb, K, CDA_SHARE, s);
+        const int lr = launch_rs_decode(d_eds, d_off, d_off + 1, d_pres, 1, K, CDA_SHARE, s);
         if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
       }
-      // verification: own axis, then orthogonal axes, per operation in order
-      std::vector<int> vaxes;
-      for (size_t q = b0; q < b1; q++) {
-        vaxes.push_back(enc_axis(ops[q].axis, ops[q].idx));
-        for (int o : ops[q].ortho) vaxes.push_back(o);
-      }
-      for (size_t v0 = 0; v0 < vaxes.size(); v0 += trees_cap) {  // chunks of at most trees_cap trees
-        std::vector<int> chunk(vaxes.begin() + v0, vaxes.begin() + std::min(vaxes.size(), v0 + trees_cap));
-        if (int r2 = roots_of(chunk)) return r2;
-        for (size_t u = 0; u < chunk.size(); u++)
-          if (!root_ok(u, chunk[u])) {
-            *bad = chunk[u];
-            return CDA_E_BYZANTINE;
-          }
-      }
-      return CDA_OK;
-    };
-    auto apply = [&](size_t q) {
-      const int axis = ops[q].axis, idx = ops[q].idx;
-      for (int j = 0; j < w; j++) {
-        uint8_t& v = P[cell(axis, idx, j)];
-        if (!v) {
-          v = 1;
-          pcnt[1 - axis][j]++;
-        }
-      }
-      pcnt[axis][idx] = w;
-    };
-    size_t b0 = 0;
-    while (b0 < ops.size()) {
-      size_t b1 = b0;
-      while (b1 < ops.size() && b1 - b0 < trees_cap / 2 && pcnt[ops[b1].axis][ops[b1].idx] >= K) b1++;
-      if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
-      int bad = 0;
-      rc = run_ops(b0, b1, &bad);
-      if (rc == CDA_E_BYZANTINE && b1 - b0 > 1) {
-        for (size_t q = b0; q < b1; q++) {  // sequential replay of the failed batch
-          rc = run_ops(q, q + 1, &bad);
-          if (rc == CDA_E_BYZANTINE) return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
-          if (rc) return rc;
-          apply(q);
-        }
-      } else {
-        if (rc == CDA_E_BYZANTINE) return finish(CDA_E_BYZANTINE, bad >> 24, bad & 0xFFFFFF);
-        if (rc) return rc;
-        for (size_t q = b0; q < b1; q++) apply(q);
-      }
-      b0 = b1;
+      std::vector<int> vaxes{enc_axis(ops[q].axis, ops[q].idx)};
+      for (int o : ops[q].ortho) vaxes.push_back(o);
+      if ((rc = roots_of(vaxes))) return rc;
+      for (size_t u = 0; u < vaxes.size(); u++)
+        if (!root_ok(u, vaxes[u])) return finish(CDA_E_BYZANTINE, vaxes[u] >> 24, vaxes[u] & 0xFFFFFF);
+      P.fill(ops[q].axis, ops[q].idx);
     }
-    if (solved) break;
-    if (!progress) return finish(CDA_E_UNREPAIRABLE, -1, -1);
+    // the replay passed: P equals the optimistic presence after batch b again, so the remaining
+    // batches' descriptors still hold; run them again on the replayed square
+    if (b + 1 < nbat) {
+      if (!dev_ok(c, hipMemsetAsync(d_bfl + b + 1, 0xFF, (nbat - b - 1) * 4, s), "memset")) return CDA_E_DEVICE;
+      if ((rc = enqueue_batches(b + 1))) return rc;
+    }
+    b++;
   }
-  return finish(CDA_OK, -1, -1);
+  return finish(solved ? CDA_OK : CDA_E_UNREPAIRABLE, -1, -1);
 }
 
 int cda_profile_enable(cda_ctx* c, int enable) {

@@ -435,6 +435,104 @@ int launch_parity_compare(const uint8_t* d_eds, int k, const int* d_axes, int na
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Repair's root check on the device: tree t (axis code axes[t]) passes iff its status word is clean
+// and its 90-B root equals want[axis][index]; *flag = min(flag, base + t) over failing trees, so
+// the flag holds the first failure in verification order.
+__global__ void __launch_bounds__(256) roots_check_kernel(const uint8_t* __restrict__ recs,
+                                                          const unsigned long long* __restrict__ st,
+                                                          const int* __restrict__ axes, int n,
+                                                          const uint8_t* __restrict__ want_rows,
+                                                          const uint8_t* __restrict__ want_cols,
+                                                          unsigned* __restrict__ flag, unsigned base) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int ax = axes[t] >> 24, idx = axes[t] & 0xFFFFFF;
+  const uint8_t* w = (ax == CDA_AXIS_ROW ? want_rows : want_cols) + (size_t)idx * CDA_NODE_SIZE;
+  const uint8_t* r = recs + (size_t)t * CDA_REC_BYTES;
+  unsigned diff = st[t] != ~0ull ? 1u : 0u;
+  for (int i = 0; i < CDA_NODE_SIZE; i++) diff |= (unsigned)(r[i] ^ w[i]);
+  if (diff) atomicMin(flag, base + (unsigned)t);
+}
+
+// Repair verification in one launch: one workgroup per axis tree.  The w leaf records are built
+// in LDS, the levels fold in place there (level l node i at slot i << l, a barrier between
+// levels), and the root is compared with want[axis][index]; a push-order violation (Q0 namespace
+// decreasing) or a differing root sets *flag = min(*flag, base + tree) (per_tree: flag[tree] = 1).  Replaces the leaf
+// kernel + log2(w) level launches + check of the generic path with one launch whose serial depth
+// is the same log2(w) node hashes.
+__global__ void __launch_bounds__(256) axes_verify_kernel(const uint8_t* __restrict__ eds, int k, int log2w,
+                                                          const int* __restrict__ axes,
+                                                          const uint8_t* __restrict__ want_rows,
+                                                          const uint8_t* __restrict__ want_cols,
+                                                          unsigned* __restrict__ flag, unsigned base,
+                                                          int per_tree) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lnodes[];  // [w][6]
+  __shared__ unsigned bad;
+  const int w = 1 << log2w;
+  const int t = blockIdx.x;
+  const int code = axes[t];
+  const int ax = code >> 24, idx = code & 0xFFFFFF;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < w; i += blockDim.x) {
+    const size_t cell = ax == CDA_AXIS_ROW ? ((size_t)idx << log2w) + i : ((size_t)i << log2w) + idx;
+    const bool q0 = (i < k) && (idx < k);
+    const uint4* sh = reinterpret_cast<const uint4*>(eds + cell * CDA_SHARE);
+    uint32_t A[16];
+    load16(sh, A);
+    if (q0 && i + 1 < k) {
+      const size_t nxt = ax == CDA_AXIS_ROW ? cell + 1 : cell + w;
+      const uint4* p = reinterpret_cast<const uint4*>(eds + nxt * CDA_SHARE);
+      uint4 v0 = p[0], v1 = p[1];
+      uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (ns_cmp(nb, A) < 0) bad = 1;
+    }
+    leaf_record(sh, A, q0, lnodes + (size_t)i * 6);
+  }
+  __syncthreads();
+  for (int l = 1; l <= log2w; l++) {
+    for (int i = threadIdx.x; i < (w >> l); i += blockDim.x)
+      hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
+                    lnodes + ((size_t)i << l) * 6);
+    __syncthreads();
+  }
+  if (threadIdx.x < 64) {  // root (slot 0) against the committed root: one 90-B compare, a wave's lanes
+    const uint8_t* r = reinterpret_cast<const uint8_t*>(lnodes);
+    const uint8_t* wr = (ax == CDA_AXIS_ROW ? want_rows : want_cols) + (size_t)idx * CDA_NODE_SIZE;
+    unsigned d = 0;
+    for (int i = threadIdx.x; i < CDA_NODE_SIZE; i += 64) d |= (unsigned)(r[i] ^ wr[i]);
+    if (threadIdx.x == 0) d |= bad;
+    if (__any(d != 0) && threadIdx.x == 0) {
+      if (per_tree) flag[t] = 1u;
+      else atomicMin(flag, base + (unsigned)t);
+    }
+  }
+}
+
+int launch_axes_verify(const uint8_t* d_eds, int k, const int* d_axes, int ntrees, const uint8_t* d_want_rows,
+                       const uint8_t* d_want_cols, unsigned* d_flag, unsigned base, bool per_tree, hipStream_t s) {
+  if (ntrees <= 0) return 0;
+  int log2w = 0;
+  while ((1 << log2w) < 2 * k) log2w++;
+  const size_t lds = ((size_t)2 * k) * CDA_REC_BYTES;
+  if (lds > 160 * 1024) return -2;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)axes_verify_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  hipLaunchKernelGGL(axes_verify_kernel, dim3(ntrees), dim3(256), lds, s, d_eds, k, log2w, d_axes, d_want_rows,
+                     d_want_cols, d_flag, base, per_tree ? 1 : 0);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_roots_check(const void* d_recs, const unsigned long long* d_status, const int* d_axes, int n,
+                       const uint8_t* d_want_rows, const uint8_t* d_want_cols, unsigned* d_flag, unsigned base,
+                       hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(roots_check_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)d_recs, d_status,
+                     d_axes, n, d_want_rows, d_want_cols, d_flag, base);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_level_generic(const void* d_in, void* d_out, int n_in, hipStream_t s) {
   const int n_out = (n_in + 1) / 2;
   hipLaunchKernelGGL(level_generic_kernel, dim3((n_out + 255) / 256), dim3(256), 0, s, (const uint4*)d_in,

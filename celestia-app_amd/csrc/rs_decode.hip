@@ -168,7 +168,7 @@ __device__ __forceinline__ unsigned cpoly_of_log(const DecArgs& a, unsigned l) {
 }
 
 template <int PL, bool INVERSE>
-__device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int log2D) {
+__device__ __forceinline__ void layer(uint32_t* st, const uint16_t* ctab, const DecArgs& a, int D, int log2D) {
   const int U = a.U, nU = a.n << a.log2U;
   const int nbu = (a.n >> 1) << a.log2U;
   for (int bu = threadIdx.x; bu < nbu; bu += blockDim.x) {
@@ -176,7 +176,7 @@ __device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int
     const int s0 = (p >> log2D) << (log2D + 1);
     const int x = s0 | (p & (D - 1));
     const int y = x + D;
-    const unsigned lm = a.skew[s0 + D - 1];
+    const unsigned cm = ctab[s0 + D - 1];  // alpha^skew in the standard basis, 0 = skip
     uint32_t X[PL], Y[PL];
 #pragma unroll
     for (int j = 0; j < PL; j++) {
@@ -186,9 +186,9 @@ __device__ __forceinline__ void layer(uint32_t* st, const DecArgs& a, int D, int
     if (INVERSE) {
 #pragma unroll
       for (int j = 0; j < PL; j++) Y[j] ^= X[j];
-      if (lm != Field<PL>::kMod) muladd_lane<PL>(X, Y, a.apow[lm]);
+      if (cm) muladd_lane<PL>(X, Y, cm);
     } else {
-      if (lm != Field<PL>::kMod) muladd_lane<PL>(X, Y, a.apow[lm]);
+      if (cm) muladd_lane<PL>(X, Y, cm);
 #pragma unroll
       for (int j = 0; j < PL; j++) Y[j] ^= X[j];
     }
@@ -207,6 +207,8 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
   uint32_t* st = smem;  // [PL][n][U] plane-major: a wave's accesses within a plane are contiguous
   uint16_t* errl = reinterpret_cast<uint16_t*>(smem + (size_t)a.n * PL * a.U);  // [n]
   uint16_t* elist = errl + a.n;                                                // [n]
+  uint16_t* ltab = elist + a.n;  // [n] log table for p ^ j < n
+  uint16_t* ctab = ltab + a.n;   // [n] FFT layer constants: apow[skew[i]], 0 where skew[i] = mod (no multiply)
   __shared__ int ecount;
   const int U = a.U, nU = a.n << a.log2U;
   int wg = blockIdx.x;
@@ -216,22 +218,25 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
   uint8_t* base = a.base + a.off[cw] + (long long)slice * U * (PL * 4);
   const long long sstride = a.stride[cw];
 
-  // erasure set in n-space
-  if (threadIdx.x == 0) {
-    int c = 0;
-    for (int i = 0; i < a.m; i++)
-      if (i >= a.k || !pres[a.k + i]) elist[c++] = (uint16_t)i;
-    for (int i = 0; i < a.k; i++)
-      if (!pres[i]) elist[c++] = (uint16_t)(a.m + i);
-    ecount = c;
+  // erasure set in n-space, gathered in parallel (its order is irrelevant: errLocs sums over it)
+  if (threadIdx.x == 0) ecount = 0;
+  for (int i = threadIdx.x; i < a.n; i += blockDim.x) {
+    ltab[i] = a.log_t[i];
+    const unsigned sk = i + 1 < a.n ? a.skew[i] : Field<PL>::kMod;  // layers read indices <= n - 2
+    ctab[i] = sk == Field<PL>::kMod ? 0 : a.apow[sk];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.m + a.k; i += blockDim.x) {
+    const bool erased = i < a.m ? (i >= a.k || !pres[a.k + i]) : !pres[i - a.m];
+    if (erased) elist[atomicAdd(&ecount, 1)] = (uint16_t)i;
   }
   __syncthreads();
   const int ne = ecount;
   for (int p = threadIdx.x; p < a.m + a.k; p += blockDim.x) {
-    unsigned long long acc = 0;
+    unsigned acc = 0;  // ne < 2^11 terms below 2^16: no overflow
     for (int t = 0; t < ne; t++) {
       const int j = elist[t];
-      if (j != p) acc += a.log_t[p ^ j];
+      acc += j != p ? ltab[p ^ j] : 0u;
     }
     errl[p] = (uint16_t)(acc % Field<PL>::kMod);
   }
@@ -255,7 +260,7 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
     for (int j = 0; j < PL; j++) st[j * nU + p * U + u] = v[j];
   }
   __syncthreads();
-  for (int lD = 0; lD < a.log2n; lD++) layer<PL, true>(st, a, 1 << lD, lD);
+  for (int lD = 0; lD < a.log2n; lD++) layer<PL, true>(st, ctab, a, 1 << lD, lD);
   // formal derivative (out of place through registers; <= 4 items per thread)
   {
     uint32_t nv[4][PL];
@@ -287,7 +292,7 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
     }
     __syncthreads();
   }
-  for (int lD = a.log2n - 1; lD >= 0; lD--) layer<PL, false>(st, a, 1 << lD, lD);
+  for (int lD = a.log2n - 1; lD >= 0; lD--) layer<PL, false>(st, ctab, a, 1 << lD, lD);
   // reveal erasures: missing shard(p) = work[p] * exp(-errLocs[p])
   for (int e = threadIdx.x; e < (a.n << a.log2U); e += blockDim.x) {
     const int p = e >> a.log2U, u = e & (U - 1);
@@ -391,7 +396,7 @@ int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d
   a.U = U;
   a.log2U = dec::ilog2(U);
   a.slices = units / U;
-  const size_t lds = (size_t)a.n * PL * U * 4 + (size_t)a.n * 4;
+  const size_t lds = (size_t)a.n * PL * U * 4 + (size_t)a.n * 8;
   if (lds > (size_t)kDecMaxLds) return -2;
   const long long grid = (long long)ncw * a.slices;
   if (grid > 0x7FFFFFFF) return -2;
