@@ -42,7 +42,7 @@ EXPORTS = [
     "cda_init", "cda_free", "cda_strerror", "cda_last_device_error",
     "cda_rs_encode", "cda_rs_decode", "cda_rs_max_chunks", "cda_rs_name", "cda_rs_validate_chunk_size",
     "cda_extend_commit", "cda_extend_commit_batch", "cda_extend_commit_device", "cda_commit_eds",
-    "cda_dah_hash", "cda_nmt_axis_root", "cda_repair",
+    "cda_dah_hash", "cda_nmt_axis_root", "cda_repair", "cda_repair_device",
     "cda_rs_encode_device", "cda_nmt_roots_device", "cda_nmt_fold_device", "cda_dah_device",
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
     "cda_blob_commitments", "cda_merkle_roots", "cda_extend_commit_nodes", "cda_share_inclusion_proof",
@@ -107,6 +107,7 @@ def lib():
                 "cda_dah_hash": (I32, [P, U32, P, P, P]),
                 "cda_nmt_axis_root": (I32, [P, U64, U64, U32, U32, P, P, P]),
                 "cda_repair": (I32, [P, U32, P, P, P, P, P]),
+                "cda_repair_device": (I32, [P, U32, P, P, P, P, P, P]),
                 "cda_rs_encode_device": (I32, [P, U32, U32, U32, P, I64, I64, P, I64, I64, P]),
                 "cda_nmt_roots_device": (I32, [P, U32, P, U32, U32, U32, U32, U32, P, P, P]),
                 "cda_nmt_fold_device": (I32, [P, U32, U32, P, P, P]),
@@ -328,6 +329,20 @@ class Context:
         rc = lib().cda_repair(self._h, w // 2, _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots, np.uint8)),
                               _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err))
         return rc, eds, pres, err
+
+    def repair_device(self, k, d_eds, present, row_roots, col_roots, stream=None):
+        """cda_repair_device: repairs the square at device address d_eds (4k^2 x 512 B) in place.
+        -> (rc, present, err); present is a repaired copy of the caller's flags."""
+        pres = np.ascontiguousarray(present, np.uint8).copy()
+        w = 2 * k
+        if pres.size != w * w or len(row_roots) != w or len(col_roots) != w:
+            raise CdaError(E_ARG, "present must hold (2k)^2 flags and the roots 2k entries each")
+        err = ErrInfo()
+        rc = lib().cda_repair_device(self._h, k, ctypes.c_void_p(d_eds), _p(pres),
+                                     _p(np.ascontiguousarray(row_roots, np.uint8)),
+                                     _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err),
+                                     ctypes.c_void_p(stream or 0))
+        return rc, pres, err
 
     # ---- blob share commitments, node export, proofs ----
     def blob_commitments(self, namespaces, datas, share_versions=None, subtree_root_threshold=64):

@@ -841,16 +841,12 @@ struct Presence {
 }  // namespace
 }  // extern "C++"
 
-int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
-               const uint8_t* col_roots, cda_err_info* err) {
-  set_err(err, CDA_OK, -1, -1, -1, -1);
-  if (!c || !eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
-  if (!is_pow2(k)) return CDA_E_NOT_POW2;
-  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
-  Lock l(c);
+// Repair of the square in host memory `eds` (uploaded, repaired, copied back) or, when eds is null,
+// of the square already in device memory d_eds_in; the caller holds the lock for stream s.
+static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, uint8_t* present,
+                       const uint8_t* row_roots, const uint8_t* col_roots, cda_err_info* err, hipStream_t s) {
   const int w = (int)(2 * k), K = (int)k;
   const size_t ncell = (size_t)w * w, eds_b = ncell * CDA_SHARE;
-  hipStream_t s = c->stream;
   int rc;
   // Generic verification workspace (sequential replay, CDA_REPAIR_FUSED=0): leaf / level records
   // for up to 4w trees.  Repair descriptors (device, staged in pinned host memory at the same
@@ -864,14 +860,14 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
   const size_t o_off = 0, o_str = o_off + 2 * W * 8, o_pres = o_str + 2 * W * 8, o_ax = o_pres + 2 * W * W,
                o_sax = o_ax + 4 * W * 4, o_all = o_sax + 2 * W * 4, o_bfl = o_all + 2 * W * 4,
                o_sfl = o_bfl + 2 * W * 4, o_pfl = o_sfl + 2 * W * 4, desc_b = o_pfl + 2 * W * 4;
-  if ((rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->ods, eds_b)) ||
+  if ((eds && (rc = ensure(c, c->eds, eds_b))) || (rc = ensure(c, c->ods, eds_b)) ||
       (rc = ensure(c, c->leaf, trees_cap * w * CDA_REC_BYTES)) ||
       (rc = ensure(c, c->scratch, trees_cap * w * CDA_REC_BYTES)) ||
       (rc = ensure(c, c->roots, trees_cap * CDA_REC_BYTES)) || (rc = ensure(c, c->status, trees_cap * 8 + 64)) ||
       (rc = ensure(c, c->dah, trees_cap * (16 + W) + 64)) || (rc = ensure(c, c->rdesc, want_b + desc_b)) ||
       (rc = ensure_host(c, c->rstage, desc_b)))
     return rc;
-  uint8_t* d_eds = (uint8_t*)c->eds.p;
+  uint8_t* d_eds = eds ? (uint8_t*)c->eds.p : d_eds_in;
   uint8_t* d_par = (uint8_t*)c->ods.p;
   const uint8_t* d_want = (const uint8_t*)c->rdesc.p;
   uint8_t* h = (uint8_t*)c->rstage.p;
@@ -882,11 +878,19 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
   const unsigned* pfl = (const unsigned*)(h + o_pfl);
   // The EDS upload (pageable memory: the copy occupies the calling thread) runs on a helper thread
   // while this one plans the whole repair on the presence bitsets.
-  bool h2d_ok = false;
-  std::thread h2d([&] {
-    (void)hipSetDevice(c->device);
-    h2d_ok = hipMemcpyAsync(d_eds, eds, eds_b, hipMemcpyHostToDevice, s) == hipSuccess;
-  });
+  bool h2d_ok = true;
+  std::thread h2d;
+  if (eds)
+    h2d = std::thread([&] {
+      (void)hipSetDevice(c->device);
+      h2d_ok = hipMemcpyAsync(d_eds, eds, eds_b, hipMemcpyHostToDevice, s) == hipSuccess;
+    });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } joiner{h2d};
   Presence P;
   P.init(w, present);
   const uint8_t* want[2] = {row_roots, col_roots};
@@ -969,7 +973,7 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
     ((int*)(h + o_all))[i] = enc_axis(CDA_AXIS_ROW, i);
     ((int*)(h + o_all))[w + i] = enc_axis(CDA_AXIS_COL, i);
   }
-  h2d.join();
+  if (h2d.joinable()) h2d.join();
   if (!h2d_ok) {
     c->last_err = "H2D failed";
     return CDA_E_DEVICE;
@@ -1016,7 +1020,7 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
     return memcmp(recs.data() + t * CDA_REC_BYTES, want[axis] + (size_t)idx * CDA_NODE_SIZE, CDA_NODE_SIZE) == 0;
   };
   auto finish = [&](int code, int axis, int idx) -> int {
-    if (!dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H")) return CDA_E_DEVICE;
+    if (eds && !dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H")) return CDA_E_DEVICE;
     for (int r = 0; r < w; r++) P.bytes(CDA_AXIS_ROW, r, present + (size_t)r * w);
     if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
     flush_profile(c);
@@ -1184,6 +1188,26 @@ int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uin
     b++;
   }
   return finish(solved ? CDA_OK : CDA_E_UNREPAIRABLE, -1, -1);
+}
+
+int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+               const uint8_t* col_roots, cda_err_info* err) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
+  Lock l(c);
+  return repair_impl(c, k, eds, nullptr, present, row_roots, col_roots, err, c->stream);
+}
+
+int cda_repair_device(cda_ctx* c, uint32_t k, void* d_eds, uint8_t* present, const uint8_t* row_roots,
+                      const uint8_t* col_roots, cda_err_info* err, void* stream) {
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !d_eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
+  if (!is_pow2(k)) return CDA_E_NOT_POW2;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
+  DevLock l(c, (hipStream_t)stream);
+  return repair_impl(c, k, nullptr, (uint8_t*)d_eds, present, row_roots, col_roots, err, (hipStream_t)stream);
 }
 
 int cda_profile_enable(cda_ctx* c, int enable) {

@@ -192,6 +192,12 @@ int cda_nmt_axis_root(cda_ctx* ctx, uint64_t square_size, uint64_t axis_index, u
  * CDA_E_BYZANTINE (err->axis/index). */
 int cda_repair(cda_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, cda_err_info* err);
+/* The same on a square already in device memory of this ctx's GPU (d_eds, 4k^2*512 bytes, repaired
+ * in place; e.g. assembled there by a sampling / reconstruction pipeline, or the output of
+ * cda_extend_commit_device).  present / roots / err are host memory.  Ordered after prior work on
+ * `stream` (0 = the null stream); returns when the repair is complete. */
+int cda_repair_device(cda_ctx* ctx, uint32_t k, void* d_eds, uint8_t* present, const uint8_t* row_roots,
+                      const uint8_t* col_roots, cda_err_info* err, void* stream);
 
 /* ---- blob share commitments (x/blob, go-square inclusion) -------------- */
 /* inclusion.CreateCommitments(blobs, merkle.HashFromByteSlices, threshold)

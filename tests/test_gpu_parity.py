@@ -576,6 +576,53 @@ def test_device_and_sync_calls_share_the_workspace():
     assert out.returncode == 0 and "workspace ok" in out.stdout, out.stderr[-3000:]
 
 
+_REPAIR_DEVICE_SCRIPT = r"""
+import sys
+import numpy as np
+import torch  # first: libcda then resolves HIP through torch's runtime, as in bench.py
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import cda
+import oracle_lib as O
+ctx = cda.Context(0)
+dev = torch.device("cuda", 0)
+s = torch.cuda.Stream(dev)
+cases = [(16, 0.6, 0, 1), (32, 0.55, 1, 2), (128, 0.5, 0, 3), (128, 0.6, 2, 4), (128, 0.25, 0, 5)]
+for k, frac, nbad, seed in cases:
+    w = 2 * k
+    rc, eds, rr, cr, _ = O.extend_commit(O.gen_ods(k, 700 + seed))
+    rng = np.random.default_rng(seed)
+    pres = (rng.random(w * w) < frac).astype(np.uint8)
+    bad = eds.copy()
+    for idx in rng.choice(np.flatnonzero(pres), nbad, replace=False):
+        bad[idx, rng.integers(0, 512)] ^= 1 + rng.integers(0, 255)
+    rc_o, eds_o, p_o, ax_o, ix_o = O.repair(bad, pres, rr, cr)
+    d = torch.from_numpy(bad).to(dev)
+    torch.cuda.synchronize()
+    rc_g, p_g, err = ctx.repair_device(k, d.data_ptr(), pres, rr, cr, s.cuda_stream)
+    got = d.cpu().numpy()
+    assert rc_g == rc_o, (k, seed, rc_g, rc_o)
+    if rc_o == O.E_BYZANTINE:
+        assert (err.axis, err.index) == (ax_o, ix_o), (k, seed)
+    assert np.array_equal(p_g, p_o), (k, seed)
+    m = p_o.astype(bool)
+    assert np.array_equal(got[m], eds_o[m]), (k, seed)
+print("repair_device ok")
+"""
+
+
+def test_repair_device_matches_sequential():
+    """cda_repair_device on a square in HBM (torch allocation, caller stream): rc, Byzantine axis/index, presence
+    and every present cell equal the sequential oracle, for repairable, Byzantine and unrepairable squares."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "celestia-app_amd")
+    out = subprocess.run([sys.executable, "-c", _REPAIR_DEVICE_SCRIPT, pkg, here], capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0 and "repair_device ok" in out.stdout, out.stderr[-3000:]
+
+
 def test_axis_root_order_error_wins_over_push_past(ctx):
     """the reference Push validates leaf by leaf, so an order violation at leaf 3 is reported even when
     the caller pushes more than 2k leaves; a sorted over-long push reports PUSH_PAST at leaf 2k."""
