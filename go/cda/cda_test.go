@@ -13,6 +13,10 @@ import (
 	"sort"
 	"testing"
 
+	"github.com/celestiaorg/go-square/blob"
+	"github.com/celestiaorg/go-square/inclusion"
+	"github.com/celestiaorg/go-square/merkle"
+	appns "github.com/celestiaorg/go-square/namespace"
 	"github.com/celestiaorg/rsmt2d"
 	"github.com/stretchr/testify/require"
 
@@ -174,4 +178,31 @@ func BenchmarkExtendShares(b *testing.B) {
 			_, _ = eds.RowRoots()
 		}
 	})
+}
+
+// TestCreateCommitmentsMatchGoSquare: one batched GPU call against go-square's inclusion.CreateCommitment per blob
+// (x/blob/types/blob_tx.go:98), over blob sizes that give 1 share up to multi-row mountains, at the default
+// subtree root threshold and a small one.
+func TestCreateCommitmentsMatchGoSquare(t *testing.T) {
+	ctx, err := cda.Default()
+	require.NoError(t, err)
+	r := rand.New(rand.NewSource(11))
+	sizes := []int{1, 478, 479, 1000, 4096, 65536, 200000, 1 << 20}
+	for _, threshold := range []int{64, 8} {
+		blobs := make([]*blob.Blob, len(sizes))
+		for i, n := range sizes {
+			id := make([]byte, appns.NamespaceVersionZeroIDSize)
+			r.Read(id)
+			data := make([]byte, n)
+			r.Read(data)
+			blobs[i] = blob.New(appns.MustNewV0(id), data, 0)
+		}
+		got, err := cda.CreateBlobCommitments(ctx, blobs, threshold)
+		require.NoError(t, err)
+		for i, b := range blobs {
+			want, err := inclusion.CreateCommitment(b, merkle.HashFromByteSlices, threshold)
+			require.NoError(t, err)
+			require.Equal(t, want, got[i], "blob %d (%d bytes), threshold %d", i, sizes[i], threshold)
+		}
+	}
 }
