@@ -93,8 +93,8 @@ func CreateBlobCommitments(ctx *Context, blobs []*blob.Blob, subtreeRootThreshol
 }
 
 // CreateCommitment is go-square inclusion.CreateCommitment for one blob.
-func CreateCommitment(ctx *Context, blob BlobRef, subtreeRootThreshold int) ([]byte, error) {
-	c, err := CreateCommitments(ctx, []BlobRef{blob}, subtreeRootThreshold)
+func CreateCommitment(ctx *Context, b BlobRef, subtreeRootThreshold int) ([]byte, error) {
+	c, err := CreateCommitments(ctx, []BlobRef{b}, subtreeRootThreshold)
 	if err != nil {
 		return nil, err
 	}
