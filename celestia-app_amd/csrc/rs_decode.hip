@@ -201,6 +201,63 @@ __device__ __forceinline__ void layer(uint32_t* st, const uint16_t* ctab, const 
   __syncthreads();
 }
 
+// Two consecutive layers (D and 2D) per LDS round trip: a thread holds the quad x0, x0+D, x0+2D, x0+3D of one
+// unit (x0 with bits log2D and log2D+1 clear).  IFFT order: layer D then 2D; FFT order: 2D then D.  Constants as in
+// layer(): group s0 + D - 1 for layer D (two groups in the quad), s0 + 2D - 1 for layer 2D (one group).
+template <int PL, bool INVERSE>
+__device__ __forceinline__ void bfly_lane(uint32_t (&X)[PL], uint32_t (&Y)[PL], unsigned c) {
+  if (INVERSE) {
+#pragma unroll
+    for (int j = 0; j < PL; j++) Y[j] ^= X[j];
+    if (c) muladd_lane<PL>(X, Y, c);
+  } else {
+    if (c) muladd_lane<PL>(X, Y, c);
+#pragma unroll
+    for (int j = 0; j < PL; j++) Y[j] ^= X[j];
+  }
+}
+
+template <int PL, bool INVERSE>
+__device__ __forceinline__ void layer4(uint32_t* st, const uint16_t* ctab, const DecArgs& a, int log2D) {
+  const int U = a.U, nU = a.n << a.log2U, D = 1 << log2D;
+  const int nq = (a.n >> 2) << a.log2U;
+  for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+    const int p4 = q >> a.log2U, u = q & (U - 1);
+    const int s0 = (p4 >> log2D) << (log2D + 2);
+    const int x0 = s0 | (p4 & (D - 1));
+    uint32_t E0[PL], E1[PL], E2[PL], E3[PL];
+#pragma unroll
+    for (int j = 0; j < PL; j++) {
+      uint32_t* b = st + j * nU + u;
+      E0[j] = b[x0 * U];
+      E1[j] = b[(x0 + D) * U];
+      E2[j] = b[(x0 + 2 * D) * U];
+      E3[j] = b[(x0 + 3 * D) * U];
+    }
+    const unsigned cA = ctab[s0 + D - 1], cB = ctab[s0 + 3 * D - 1], cC = ctab[s0 + 2 * D - 1];
+    if (INVERSE) {
+      bfly_lane<PL, true>(E0, E1, cA);
+      bfly_lane<PL, true>(E2, E3, cB);
+      bfly_lane<PL, true>(E0, E2, cC);
+      bfly_lane<PL, true>(E1, E3, cC);
+    } else {
+      bfly_lane<PL, false>(E0, E2, cC);
+      bfly_lane<PL, false>(E1, E3, cC);
+      bfly_lane<PL, false>(E0, E1, cA);
+      bfly_lane<PL, false>(E2, E3, cB);
+    }
+#pragma unroll
+    for (int j = 0; j < PL; j++) {
+      uint32_t* b = st + j * nU + u;
+      b[x0 * U] = E0[j];
+      b[(x0 + D) * U] = E1[j];
+      b[(x0 + 2 * D) * U] = E2[j];
+      b[(x0 + 3 * D) * U] = E3[j];
+    }
+  }
+  __syncthreads();
+}
+
 template <int PL>
 __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -260,7 +317,13 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
     for (int j = 0; j < PL; j++) st[j * nU + p * U + u] = v[j];
   }
   __syncthreads();
-  for (int lD = 0; lD < a.log2n; lD++) layer<PL, true>(st, ctab, a, 1 << lD, lD);
+  {  // IFFT: layers D = 1, 2, 4, ... (GF(2^8): two per LDS round trip; GF(2^16) keeps one, its quad
+     // state would cost 180 VGPRs)
+    int lD = 0;
+    if (PL == 8)
+      for (; lD + 1 < a.log2n; lD += 2) layer4<PL, true>(st, ctab, a, lD);
+    for (; lD < a.log2n; lD++) layer<PL, true>(st, ctab, a, 1 << lD, lD);
+  }
   // formal derivative (out of place through registers; <= 4 items per thread)
   {
     uint32_t nv[4][PL];
@@ -292,7 +355,17 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
     }
     __syncthreads();
   }
-  for (int lD = a.log2n - 1; lD >= 0; lD--) layer<PL, false>(st, ctab, a, 1 << lD, lD);
+  {  // FFT: layers D = n/2, ..., 2, 1 (GF(2^8): an odd top layer alone, then pairs (2D, D))
+    int top = a.log2n - 1;
+    if (PL == 8) {
+      if (a.log2n & 1) {
+        layer<PL, false>(st, ctab, a, 1 << top, top);
+        top--;
+      }
+      for (; top >= 1; top -= 2) layer4<PL, false>(st, ctab, a, top - 1);
+    }
+    for (; top >= 0; top--) layer<PL, false>(st, ctab, a, 1 << top, top);
+  }
   // reveal erasures: missing shard(p) = work[p] * exp(-errLocs[p])
   for (int e = threadIdx.x; e < (a.n << a.log2U); e += blockDim.x) {
     const int p = e >> a.log2U, u = e & (U - 1);

@@ -508,6 +508,32 @@ def test_repair_byzantine_random_matches_sequential(ctx, k, frac, nbad, seed):
     _check_repair_exact(ctx, bad, pres, rr, cr)
 
 
+def test_repair_randomised_sweep_matches_sequential(ctx):
+    """Stress for the optimistic whole-repair execution (every sweep planned up front, one host wait, sequential
+    replay from the first failing batch): 48 random squares, k = 4..64, survival 20..85 %, 0..3 corrupted present
+    cells, some in complete rows / columns (sanity check) -- rc, axis/index, presence and present cells equal the
+    sequential oracle in every case."""
+    rng = np.random.default_rng(2024)
+    outcomes = set()
+    for case in range(48):
+        k = int(rng.choice([4, 8, 16, 32, 64]))
+        w = 2 * k
+        eds, rr, cr = _square(k, 3000 + case)
+        frac = float(rng.uniform(0.2, 0.85))
+        pres = (rng.random(w * w) < frac).astype(np.uint8)
+        if case % 6 == 0:  # complete a few rows so the sanity check has work
+            for r in rng.choice(w, 2, replace=False):
+                pres[r * w:(r + 1) * w] = 1
+        bad = eds.copy()
+        nbad = int(rng.integers(0, 4))
+        if nbad and pres.any():
+            for idx in rng.choice(np.flatnonzero(pres), min(nbad, int(pres.sum())), replace=False):
+                bad[idx, rng.integers(0, 512)] ^= 1 + rng.integers(0, 255)
+        rc, _ = _check_repair_exact(ctx, bad, pres, rr, cr)
+        outcomes.add(rc)
+    assert {0, O.E_BYZANTINE, O.E_UNREPAIRABLE} <= outcomes, outcomes
+
+
 def test_compute_eds_honours_custom_tree_constructor(ctx):
     """A TreeConstructorFn other than wrapper.NewConstructor is called the rsmt2d way:
     one tree per axis, the axis's cells pushed in order; the roots are the custom trees' roots."""
