@@ -6,7 +6,8 @@
  * tests/golden/oracle_digests.json and mainnet block 408's data_hash.
  *
  *   abi_host_client <ods.bin> <k> <out_dir>
- * writes <out_dir>/{eds,row_roots,col_roots,dah,parity,repaired}.bin and prints one status line.
+ * writes <out_dir>/{eds,row_roots,col_roots,dah,parity,repaired,commitments}.bin and prints one status line.
+ * Also checked in-process: Codec.Decode of an erased row, a wrapper tree root, the multi-device batch.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -98,7 +99,55 @@ int main(int argc, char** argv) {
       return 1;
     }
 
-  if (write_file(argv[3], "eds.bin", eds, (size_t)w * w * S) || write_file(argv[3], "row_roots.bin", rows, (size_t)w * CDA_NODE_SIZE) ||
+  /* rsmt2d.Codec.Decode of EDS row 0 with every other shard erased (k of 2k present) */
+  uint8_t* cw = malloc((size_t)w * S);
+  uint8_t* cw_present = malloc(w);
+  memcpy(cw, eds, (size_t)w * S);
+  for (uint32_t i = 0; i < w; i++) {
+    cw_present[i] = (uint8_t)(i % 2 == 0);
+    if (!cw_present[i]) memset(cw + (size_t)i * S, 0xEE, S);
+  }
+  rc = cda_rs_decode(ctx, k, (uint32_t)S, cw, cw_present);
+  if (rc) return fail("cda_rs_decode", rc, NULL);
+  if (memcmp(cw, eds, (size_t)w * S) != 0) {
+    fprintf(stderr, "decoded row 0 differs from the EDS\n");
+    return 1;
+  }
+
+  /* wrapper.NewConstructor(k)(Row, 0): push row 0's 2k cells, Root() == the block path's row root 0 */
+  uint8_t root[CDA_NODE_SIZE];
+  rc = cda_nmt_axis_root(ctx, k, 0, w, (uint32_t)S, eds, root, &err);
+  if (rc) return fail("cda_nmt_axis_root", rc, &err);
+  if (memcmp(root, rows, CDA_NODE_SIZE) != 0) {
+    fprintf(stderr, "axis root differs from row root 0\n");
+    return 1;
+  }
+
+  /* inclusion.CreateCommitments over two blobs cut from the ODS bytes (namespace = share 0's) */
+  const uint64_t tot = (uint64_t)count * S, b1 = tot / 2 < 1000 ? tot / 2 : 1000, b2 = b1 + 5000 < tot ? b1 + 5000 : tot;
+  const uint64_t offs[3] = {0, b1, b2};
+  uint8_t ns2[2 * CDA_NAMESPACE_SIZE];
+  memcpy(ns2, ods, CDA_NAMESPACE_SIZE);
+  memcpy(ns2 + CDA_NAMESPACE_SIZE, ods, CDA_NAMESPACE_SIZE);
+  uint8_t commitments[64];
+  rc = cda_blob_commitments(ctx, 2, ns2, ods, offs, NULL, 64, commitments, &err);
+  if (rc) return fail("cda_blob_commitments", rc, &err);
+
+  /* the multi-device handle over every visible GPU: two blocks, same DAH each */
+  cda_multi* multi = NULL;
+  rc = cda_multi_init(0, &multi);
+  if (rc) return fail("cda_multi_init", rc, NULL);
+  uint8_t dahm[64];
+  rc = cda_multi_extend_commit_batch(multi, k, 2, ods3, NULL, rows3, cols3, dahm, &err);
+  if (rc) return fail("cda_multi_extend_commit_batch", rc, &err);
+  if (memcmp(dahm, dah, 32) != 0 || memcmp(dahm + 32, dah, 32) != 0) {
+    fprintf(stderr, "multi-device DAH differs\n");
+    return 1;
+  }
+  cda_multi_free(multi);
+
+  if (write_file(argv[3], "commitments.bin", commitments, sizeof commitments) ||
+      write_file(argv[3], "eds.bin", eds, (size_t)w * w * S) || write_file(argv[3], "row_roots.bin", rows, (size_t)w * CDA_NODE_SIZE) ||
       write_file(argv[3], "col_roots.bin", cols, (size_t)w * CDA_NODE_SIZE) || write_file(argv[3], "dah.bin", dah, 32) ||
       write_file(argv[3], "parity.bin", parity, (size_t)k * S) || write_file(argv[3], "repaired.bin", damaged, (size_t)w * w * S)) {
     fprintf(stderr, "cannot write outputs\n");
@@ -109,6 +158,6 @@ int main(int argc, char** argv) {
   printf("\n");
   cda_free(ctx);
   free(ods); free(eds); free(rows); free(cols); free(parity); free(damaged); free(present);
-  free(ods3); free(rows3); free(cols3);
+  free(ods3); free(rows3); free(cols3); free(cw); free(cw_present);
   return 0;
 }

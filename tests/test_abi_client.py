@@ -27,6 +27,13 @@ def _run(tmp_path, ods, k):
     assert out.returncode == 0, out.stderr
     assert "abi_host_client ok" in out.stdout
     rd = lambda n: (tmp_path / n).read_bytes()  # noqa: E731
+    flat = np.ascontiguousarray(ods, np.uint8).tobytes()
+    ns, tot = flat[:29], len(flat)
+    b1 = min(tot // 2, 1000)
+    b2 = min(b1 + 5000, tot)
+    for i, (a, b) in enumerate(((0, b1), (b1, b2))):  # the client's two blobs, against oracle/inclusion.c
+        rc, want = O.blob_commitment(ns, flat[a:b])
+        assert rc == 0 and rd("commitments.bin")[32 * i:32 * (i + 1)] == want, i
     return rd("eds.bin"), rd("row_roots.bin"), rd("col_roots.bin"), rd("dah.bin"), rd("repaired.bin")
 
 
