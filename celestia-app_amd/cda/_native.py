@@ -10,7 +10,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcda.so")
+# CDA_LIB: another build of the library (A/B measurements of kernel variants on one box)
+LIB_PATH = os.environ.get("CDA_LIB") or os.path.join(_HERE, "libcda.so")
 
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
