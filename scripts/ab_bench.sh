@@ -1,19 +1,33 @@
 #!/bin/bash
-# A/B of two library builds on one box: alternating short bench runs (no extras), kernel times per run.
-# usage: scripts/ab_bench.sh <lib_a.so> <lib_b.so> [rounds]
+# A/B/... of library builds on one box: short bench runs (no extras) in a rotating order so that run position
+# (clock / thermal drift) does not favour one build; prints each run and the per-build means of the kernel times.
+# usage: scripts/ab_bench.sh <rounds> <lib.so> [<lib.so> ...]
 set -u
-A=$1; B=$2; N=${3:-3}
+N=$1; shift
+LIBS=("$@")
+M=${#LIBS[@]}
 mkdir -p gpurun_out
-for i in $(seq 1 "$N"); do
-  for v in A B; do
-    lib=$A; [ "$v" = B ] && lib=$B
-    CDA_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > gpurun_out/ab_$v.log 2>&1 || exit 1
+: > gpurun_out/ab_runs.jsonl
+for i in $(seq 0 $((N - 1))); do
+  for j in $(seq 0 $((M - 1))); do
+    lib=${LIBS[$(((i + j) % M))]}
+    CDA_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > gpurun_out/ab_run.log 2>&1 || exit 1
     python3 -c "
 import json
-for l in open('gpurun_out/ab_$v.log'):
+for l in open('gpurun_out/ab_run.log'):
     if l.startswith('{'):
-        d=json.loads(l); k=d['kernels_ms']
-        print('$v', d['value'], d['ms_per_step'], ' '.join(f'{n}={t}' for n, t in sorted(k.items())))
-"
+        d=json.loads(l); print(json.dumps({'lib': '$lib', 'value': d['value'], 'kernels': d['kernels_ms']}))
+" >> gpurun_out/ab_runs.jsonl
+    tail -n 1 gpurun_out/ab_runs.jsonl
   done
 done
+python3 - <<'PY'
+import json, collections
+runs = [json.loads(l) for l in open('gpurun_out/ab_runs.jsonl')]
+by = collections.defaultdict(list)
+for r in runs: by[r['lib']].append(r)
+for lib, rs in by.items():
+    ks = sorted(rs[0]['kernels'])
+    mean = {k: round(sum(r['kernels'][k] for r in rs) / len(rs), 4) for k in ks}
+    print(lib, 'blocks/s', round(sum(r['value'] for r in rs) / len(rs)), mean)
+PY
