@@ -248,6 +248,42 @@ def pmc_counters(kernel, B):
     return None
 
 
+def single_block_measure(ctx, dev, k=128, reps=50):
+    """Config C2: ONE k=128 block on one GPU, device-resident (the latency of one ExtendShares +
+    NewDataAvailabilityHeader with the ODS already in HBM), with its per-kernel split.  One block fills few of the
+    256 CUs (the tree levels and the DAH are chains of dependent SHA-256 compressions), so this is latency, not the
+    batch throughput of the headline."""
+    import torch
+    w = 2 * k
+    ods = torch.from_numpy(gen_ods(k, 0xC0FFEE)).to(dev)
+    eds = torch.empty((1, w * w, 512), dtype=torch.uint8, device=dev)
+    roots = torch.empty((1, 2 * w, 96), dtype=torch.uint8, device=dev)
+    dah = torch.empty((1, 32), dtype=torch.uint8, device=dev)
+    st = torch.empty((1,), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.extend_commit_device(k, 1, ods.data_ptr(), eds.data_ptr(), roots.data_ptr(), dah.data_ptr(),
+                                 st.data_ptr(), stream.cuda_stream)
+    step()
+    torch.cuda.synchronize(dev)
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize(dev)
+        best = min(best, time.perf_counter() - t0)
+    ctx.profile_reset()
+    ctx.profile_enable(True)
+    step()
+    torch.cuda.synchronize(dev)
+    prof = ctx.profile_read()
+    ctx.profile_enable(False)
+    return {"k": k, "ms": round(best * 1e3, 3),
+            "kernels_ms": {n: round(ms / max(1, cnt), 4) for n, (ms, cnt) in prof.items()},
+            "note": "device-resident, best of %d; host-buffer latency: host_buffers.one_block_latency_ms" % reps}
+
+
 def k512_measure(ctx, dev, reps=3):
     """Config C5 on ONE GPU: k=512 (GF(2^16) Leopard, 512 MiB EDS, 2,048 roots) through the device-resident block
     path (2 blocks per call), and through cda.split with a single rank (the multi-GPU code path at world size 1).
@@ -629,6 +665,7 @@ def main():
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
     if rank == 0 and world == 1 and not args.no_extras:
+        result["c2_single_block"] = single_block_measure(ctx, dev)
         result["repair_c4"] = repair_measure(ctx)
         result["blob_commitments"] = commitments_measure(ctx)
         result["host_buffers"] = host_path_measure(ctx, k)
