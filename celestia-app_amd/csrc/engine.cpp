@@ -967,6 +967,33 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   }
   if (vall.size() > 4 * W) return CDA_E_ARG;  // cannot happen: the bound above
   const size_t nbat = bat.size();
+  // Host buffers: rows go back to the caller while later batches still run.  blast[r] = the last batch that writes
+  // a cell of row r (a row operation on r, or a column operation with (r, c) missing at its batch start); once that
+  // batch's decode has finished the row holds its final bytes if every check passes.
+  std::vector<int> blast(w, -1);
+  for (size_t b = 0; b < nbat; b++)
+    for (size_t q = bat[b].q0; q < bat[b].q1; q++) {
+      if (ops[q].axis == CDA_AXIS_ROW) {
+        blast[ops[q].idx] = (int)b;
+        continue;
+      }
+      const uint8_t* pr = h + o_pres + q * W;
+      for (int j = 0; j < w; j++)
+        if (!pr[j]) blast[j] = (int)b;
+    }
+  const bool early = eds && !c->prof && nbat > 0;
+  std::vector<hipEvent_t> bev(early ? nbat : 0, nullptr);
+  struct EventsGuard {
+    std::vector<hipEvent_t>& v;
+    ~EventsGuard() {
+      for (auto e : v)
+        if (e) (void)hipEventDestroy(e);
+    }
+  } events_guard{bev};
+  for (int r = 0; r < w && early; r++)
+    if (blast[r] >= 0 && !bev[blast[r]] &&
+        !dev_ok(c, hipEventCreateWithFlags(&bev[blast[r]], hipEventDisableTiming), "hipEventCreate"))
+      return CDA_E_DEVICE;
   memcpy(h + o_ax, vall.data(), vall.size() * 4);
   memcpy(h + o_sax, sane.data(), sane.size() * 4);
   for (int i = 0; i < w; i++) {
@@ -1019,8 +1046,19 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     if (st[t] != ~0ull) return false;  // push error => byzantine
     return memcmp(recs.data() + t * CDA_REC_BYTES, want[axis] + (size_t)idx * CDA_NODE_SIZE, CDA_NODE_SIZE) == 0;
   };
+  std::thread early_d2h;
+  bool early_ok = false, early_failed = false;  // the early rows are the answer / the copier hit an error
+  struct EarlyJoiner {
+    std::thread& t;
+    ~EarlyJoiner() {
+      if (t.joinable()) t.join();
+    }
+  } early_joiner{early_d2h};
   auto finish = [&](int code, int axis, int idx) -> int {
-    if (eds && !dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H")) return CDA_E_DEVICE;
+    if (early_d2h.joinable()) early_d2h.join();
+    if (eds && !(early_ok && !early_failed) &&
+        !dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H"))
+      return CDA_E_DEVICE;
     for (int r = 0; r < w; r++) P.bytes(CDA_AXIS_ROW, r, present + (size_t)r * w);
     if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
     flush_profile(c);
@@ -1101,6 +1139,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
                                         (int)(bt.q1 - bt.q0), K, CDA_SHARE, s);
         if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
       }
+      if (from == 0 && early && bev[b] && !dev_ok(c, hipEventRecord(bev[b], s), "hipEventRecord")) return CDA_E_DEVICE;
       hipStream_t v = vstream(b);
       if (!fork(v)) return CDA_E_DEVICE;
       const size_t nv = bt.v1 - bt.v0;
@@ -1124,12 +1163,46 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     }
     if (!join() ||
         !dev_ok(c, hipMemcpyAsync(h + o_bfl, dd + o_bfl, o_pfl + 2 * W * 4 - o_bfl, hipMemcpyDeviceToHost, s),
-                "D2H") ||
-        !dev_ok(c, hipStreamSynchronize(s), "sync"))
+                "D2H"))
       return CDA_E_DEVICE;
     return CDA_OK;
   };
   if ((rc = enqueue_batches(0))) return rc;
+  if (early)  // rows whose last writer has run go back on their own stream (pageable: from a helper thread)
+    early_d2h = std::thread([&] {
+      (void)hipSetDevice(c->device);
+      hipStream_t d2h = c->sub[cda_ctx::kMaxSub - 4];
+      const size_t row_b = W * CDA_SHARE;
+      for (size_t b = 0; b < nbat && !early_failed; b++) {
+        if (!bev[b]) continue;
+        if (hipEventSynchronize(bev[b]) != hipSuccess) {
+          early_failed = true;
+          break;
+        }
+        for (int r = 0; r < w;) {  // runs of consecutive rows finished by batch b
+          if (blast[r] != (int)b) {
+            r++;
+            continue;
+          }
+          int r1 = r;
+          while (r1 < w && blast[r1] == (int)b) r1++;
+          if (hipMemcpyAsync(eds + r * row_b, d_eds + r * row_b, (size_t)(r1 - r) * row_b, hipMemcpyDeviceToHost,
+                             d2h) != hipSuccess)
+            early_failed = true;
+          r = r1;
+        }
+      }
+      if (hipStreamSynchronize(d2h) != hipSuccess) early_failed = true;
+    });
+  if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
+  {  // the early rows are the answer when the sanity check and every batch of this first pass passed
+    bool all = true;
+    for (size_t b = 0; b < nbat; b++) all = all && bfl[b] == ~0u;
+    for (size_t t = 0; t < sane.size() && all; t++) all = c->repair_fused_verify ? sfl[t] == 0 : san_bad[t] == 0;
+    for (int i = 0; i < 2 * w && all && !sane.empty(); i++)
+      all = (i < w ? P.cnt[CDA_AXIS_ROW][i] : P.cnt[CDA_AXIS_COL][i - w]) != w || pfl[i] == 0;
+    early_ok = early && all;
+  }
 
   // sanity report in a fixed order: i ascending; row root, col root, row parity, col parity
   if (!sane.empty()) {
@@ -1184,6 +1257,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     if (b + 1 < nbat) {
       if (!dev_ok(c, hipMemsetAsync(d_bfl + b + 1, 0xFF, (nbat - b - 1) * 4, s), "memset")) return CDA_E_DEVICE;
       if ((rc = enqueue_batches(b + 1))) return rc;
+      if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
     }
     b++;
   }
