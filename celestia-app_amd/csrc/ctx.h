@@ -30,6 +30,8 @@ struct cda_ctx {
   bool repair_overlap = true;
   // CDA_REPAIR_FUSED=0: verify with the generic leaf + per-level launches instead of one fused launch
   bool repair_fused_verify = true;
+  // CDA_REPAIR_EARLY=0: repair copies the square back only at the end (no early row return)
+  bool repair_early = true;
   hipStream_t sub[kMaxSub] = {};
   // Workspace ordering across streams: the device-resident entry points enqueue on the caller's
   // stream but use this ctx's workspace (leaf/scratch records).  ws_event marks the end of the

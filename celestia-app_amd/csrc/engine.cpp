@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -344,6 +345,7 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_FUSED")) c->fused = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_OVERLAP")) c->repair_overlap = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
+  if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;
@@ -843,6 +845,30 @@ struct Presence {
 
 // Repair of the square in host memory `eds` (uploaded, repaired, copied back) or, when eds is null,
 // of the square already in device memory d_eds_in; the caller holds the lock for stream s.
+// CDA_REPAIR_TRACE=1: host-side phase times of each repair on stderr (where a slow host-buffer repair spends it)
+struct RepairTrace {
+  bool on = false;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+  std::string line;
+  RepairTrace() {
+    static const bool env = getenv("CDA_REPAIR_TRACE") && atoi(getenv("CDA_REPAIR_TRACE")) != 0;
+    on = env;
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[64];
+    snprintf(b, sizeof b, " %s=%.0f", what, std::chrono::duration<double, std::micro>(now - last).count());
+    line += b;
+    last = now;
+  }
+  ~RepairTrace() {
+    if (on)
+      fprintf(stderr, "cda_repair trace (us):%s total=%.0f\n", line.c_str(),
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+
 static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, uint8_t* present,
                        const uint8_t* row_roots, const uint8_t* col_roots, cda_err_info* err, hipStream_t s) {
   const int w = (int)(2 * k), K = (int)k;
@@ -891,6 +917,8 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
       if (t.joinable()) t.join();
     }
   } joiner{h2d};
+  RepairTrace tr;
+  tr.mark("setup");
   Presence P;
   P.init(w, present);
   const uint8_t* want[2] = {row_roots, col_roots};
@@ -981,7 +1009,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
       for (int j = 0; j < w; j++)
         if (!pr[j]) blast[j] = (int)b;
     }
-  const bool early = eds && !c->prof && nbat > 0;
+  const bool early = eds && !c->prof && nbat > 0 && c->repair_early;
   std::vector<hipEvent_t> bev(early ? nbat : 0, nullptr);
   struct EventsGuard {
     std::vector<hipEvent_t>& v;
@@ -1000,7 +1028,9 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     ((int*)(h + o_all))[i] = enc_axis(CDA_AXIS_ROW, i);
     ((int*)(h + o_all))[w + i] = enc_axis(CDA_AXIS_COL, i);
   }
+  tr.mark("plan");
   if (h2d.joinable()) h2d.join();
+  tr.mark("h2d_wait");
   if (!h2d_ok) {
     c->last_err = "H2D failed";
     return CDA_E_DEVICE;
@@ -1055,12 +1085,15 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     }
   } early_joiner{early_d2h};
   auto finish = [&](int code, int axis, int idx) -> int {
+    tr.mark("evaluate");
     if (early_d2h.joinable()) early_d2h.join();
+    tr.mark("early_join");
     if (eds && !(early_ok && !early_failed) &&
         !dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H"))
       return CDA_E_DEVICE;
     for (int r = 0; r < w; r++) P.bytes(CDA_AXIS_ROW, r, present + (size_t)r * w);
     if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
+    tr.mark("final_d2h");
     flush_profile(c);
     if (code != CDA_OK) set_err(err, code, axis, idx, -1, -1);
     return code;
@@ -1167,7 +1200,9 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
       return CDA_E_DEVICE;
     return CDA_OK;
   };
+  tr.mark("upload_rest");
   if ((rc = enqueue_batches(0))) return rc;
+  tr.mark("enqueue");
   if (early)  // rows whose last writer has run go back on their own stream (pageable: from a helper thread)
     early_d2h = std::thread([&] {
       (void)hipSetDevice(c->device);
@@ -1195,6 +1230,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
       if (hipStreamSynchronize(d2h) != hipSuccess) early_failed = true;
     });
   if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
+  tr.mark("gpu_wait");
   {  // the early rows are the answer when the sanity check and every batch of this first pass passed
     bool all = true;
     for (size_t b = 0; b < nbat; b++) all = all && bfl[b] == ~0u;
