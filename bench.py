@@ -169,9 +169,9 @@ def cpu_baseline(k, seconds):
 def repair_measure(ctx, k=128, survive=0.5, reps=5, warmup=2):
     """Config C4: rsmt2d Repair of a k=128 EDS from a random `survive` fraction of cells (host buffers in/out, repaired
     in place as through the C ABI), plus the Q0-only case (25 % of the cells: the structured repairable form of
-    BASELINE's "25 % surviving"; random 25 % is unrepairable).  The host square is one reused,
-    already-touched buffer (as host_buffers' outputs): the first pageable copies of a process run slower while the
-    HIP runtime warms up, so `warmup` untimed repairs precede the timed ones; min and median are reported."""
+    BASELINE's "25 % surviving"; random 25 % is unrepairable).  Each call gets a newly allocated
+    (written) host square, as a cgo caller's; `warmup` untimed repairs precede the timed ones; min and median are
+    reported."""
     import torch
 
     import cda
@@ -183,12 +183,12 @@ def repair_measure(ctx, k=128, survive=0.5, reps=5, warmup=2):
     q0 = np.zeros((w, w), np.uint8)
     q0[:k, :k] = 1
     d_eds = torch.empty(eds.shape, dtype=torch.uint8, device="cuda")
-    damaged = np.empty_like(eds)
     for name, mk in (("random", lambda: (rng.random(w * w) < survive).astype(np.uint8)),
                      ("q0_only", lambda: q0.reshape(-1).copy())):
         ms, dms, ok = [], [], True
         for it in range(warmup + reps):
             present = mk()
+            damaged = np.empty_like(eds)  # a new caller buffer per call, as go/cda's Repair allocates one
             np.copyto(damaged, eds)
             damaged[present == 0] = 0
             # device-resident form first (cda_repair_device on the square in HBM), then the host-buffer form
@@ -217,7 +217,7 @@ def repair_measure(ctx, k=128, survive=0.5, reps=5, warmup=2):
     out["survive"] = survive
     out["note"] = ("ms: cda_repair on host buffers, 32 MiB H2D + D2H of the EDS included (PCIe); device_resident_ms: "
                    "cda_repair_device on the square in HBM (presence and roots from the host); "
-                   f"{warmup} untimed + {reps} timed repairs per case, one reused host buffer")
+                   f"{warmup} untimed + {reps} timed repairs per case, a new host buffer per call")
     return out
 
 

@@ -10,6 +10,10 @@
 
 #include "cda_internal.h"
 
+namespace cda {
+struct Stager;  // staging.cpp
+}
+
 struct cda_ctx {
   int device = 0;
   std::recursive_mutex mu;
@@ -53,6 +57,11 @@ struct cda_ctx {
   Buf ods, eds, leaf, scratch, roots, dah, status, plan, payload;
   // repair: device root table + per-sweep descriptors, and their pinned host staging
   Buf rdesc, rstage;
+  // pinned staging rings for cda_repair's large copies of caller (pageable) memory, one per direction
+  // (staging.cpp); CDA_STAGING: bit 0 stages uploads, bit 1 downloads (0 = plain hipMemcpyAsync)
+  cda::Stager* st_in = nullptr;
+  cda::Stager* st_out = nullptr;
+  int staging = 3;
   // profiling
   bool prof = false;
   struct Pending {
@@ -87,6 +96,12 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
 int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
                     uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err, int block0);
 void free_pipeline(cda_ctx* c);
+// Caller-memory copies (staging.cpp): large pageable buffers through the pinned rings, pinned / small ones
+// directly.  staged_h2d returns once the source may be released (DMA enqueued on s); staged_d2h once the
+// bytes are in h_dst (it waits for s).
+int staged_h2d(cda_ctx* c, void* d_dst, const void* h_src, size_t n, hipStream_t s);
+int staged_d2h(cda_ctx* c, void* h_dst, const void* d_src, size_t n, hipStream_t s);
+void free_staging(cda_ctx* c);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 

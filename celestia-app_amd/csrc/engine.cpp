@@ -346,6 +346,7 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_REPAIR_OVERLAP")) c->repair_overlap = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
+  if (const char* e = getenv("CDA_STAGING")) c->staging = atoi(e) & 3;
   bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;
@@ -376,6 +377,7 @@ void cda_free(cda_ctx* c) {
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
     free_pipeline(c);
+    free_staging(c);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
     if (c->sync_ev) (void)hipEventDestroy(c->sync_ev);
@@ -909,7 +911,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   if (eds)
     h2d = std::thread([&] {
       (void)hipSetDevice(c->device);
-      h2d_ok = hipMemcpyAsync(d_eds, eds, eds_b, hipMemcpyHostToDevice, s) == hipSuccess;
+      h2d_ok = staged_h2d(c, d_eds, eds, eds_b, s) == CDA_OK;
     });
   struct Joiner {
     std::thread& t;
@@ -1088,9 +1090,10 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     tr.mark("evaluate");
     if (early_d2h.joinable()) early_d2h.join();
     tr.mark("early_join");
-    if (eds && !(early_ok && !early_failed) &&
-        !dev_ok(c, hipMemcpyAsync(eds, d_eds, eds_b, hipMemcpyDeviceToHost, s), "D2H"))
-      return CDA_E_DEVICE;
+    if (eds && !(early_ok && !early_failed)) {
+      const int r2 = staged_d2h(c, eds, d_eds, eds_b, s);
+      if (r2) return r2;
+    }
     for (int r = 0; r < w; r++) P.bytes(CDA_AXIS_ROW, r, present + (size_t)r * w);
     if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
     tr.mark("final_d2h");
@@ -1221,8 +1224,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
           }
           int r1 = r;
           while (r1 < w && blast[r1] == (int)b) r1++;
-          if (hipMemcpyAsync(eds + r * row_b, d_eds + r * row_b, (size_t)(r1 - r) * row_b, hipMemcpyDeviceToHost,
-                             d2h) != hipSuccess)
+          if (staged_d2h(c, eds + r * row_b, d_eds + r * row_b, (size_t)(r1 - r) * row_b, d2h) != CDA_OK)
             early_failed = true;
           r = r1;
         }

@@ -1,0 +1,187 @@
+// staging.cpp — host <-> device copies of caller memory through pinned staging rings (used by cda_repair).
+//
+// cda_repair moves the whole 32 MiB square up and back from helper threads (the upload overlaps the host's
+// planning, rows return while later batches run).  Issued as plain pageable hipMemcpyAsync from those
+// threads the copies were erratic on MI355X boxes: C4 with a freshly allocated caller buffer took 2.6 ms at
+// best but 15-22 ms at the median (scripts/fresh_buffer_probe.py, CDA_STAGING=0).  Through a ring of pinned
+// slots -- worker threads copy chunk i into a slot (host memcpy, ~35 GB/s with three threads) while the DMA
+// of chunk i-1 runs -- the same repair takes 2.6-2.9 ms every time.  The block paths keep plain
+// hipMemcpyAsync: there the staged copy measured 20-30 % slower (a 48-block batch with its EDS 42 vs 32 ms)
+// and the pageable copies were steady.  Pinned caller memory (cda_host_alloc, hipHostRegister) and small
+// copies go straight to hipMemcpyAsync.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ctx.h"
+
+namespace cda {
+
+struct Stager {
+  static constexpr int kSlots = 3;
+  static constexpr size_t kSlotBytes = (size_t)4 << 20;
+  static constexpr int kWorkers = 2;  // + the calling thread
+  uint8_t* ring = nullptr;            // kSlots x kSlotBytes pinned
+  hipEvent_t ev[kSlots] = {};
+  bool used[kSlots] = {};  // ev[j] has been recorded (waits on never-recorded events are skipped)
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv_work, cv_done;
+  uint8_t* jdst = nullptr;
+  const uint8_t* jsrc = nullptr;
+  size_t jn = 0;
+  unsigned gen = 0;
+  int pending = 0;
+  bool stop = false;
+
+  // part `i` of kWorkers + 1 of the current job
+  void part(int i) {
+    const size_t parts = kWorkers + 1, lo = jn * i / parts, hi = jn * (i + 1) / parts;
+    if (hi > lo) memcpy(jdst + lo, jsrc + lo, hi - lo);
+  }
+  void worker(int i) {
+    unsigned seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m);
+        cv_work.wait(g, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+      }
+      part(i);
+      {
+        std::lock_guard<std::mutex> g(m);
+        --pending;
+      }
+      cv_done.notify_one();
+    }
+  }
+  // memcpy split over the workers and the calling thread
+  void pmemcpy(void* dst, const void* src, size_t n) {
+    if (n < ((size_t)256 << 10)) {
+      memcpy(dst, src, n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m);
+      jdst = (uint8_t*)dst;
+      jsrc = (const uint8_t*)src;
+      jn = n;
+      pending = kWorkers;
+      ++gen;
+    }
+    cv_work.notify_all();
+    part(kWorkers);
+    std::unique_lock<std::mutex> g(m);
+    cv_done.wait(g, [&] { return pending == 0; });
+  }
+  ~Stager() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv_work.notify_all();
+    for (auto& t : th) t.join();
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (ring) (void)hipHostFree(ring);
+  }
+};
+
+static int get_stager(cda_ctx* c, Stager*& st) {
+  if (st) return CDA_OK;
+  auto* s = new Stager();
+  bool ok = hipHostMalloc((void**)&s->ring, Stager::kSlots * Stager::kSlotBytes, hipHostMallocDefault) == hipSuccess;
+  for (int j = 0; j < Stager::kSlots && ok; j++)
+    ok = hipEventCreateWithFlags(&s->ev[j], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    c->last_err = "staging ring allocation failed";
+    delete s;
+    return CDA_E_DEVICE;
+  }
+  for (int i = 0; i < Stager::kWorkers; i++) s->th.emplace_back([s, i] { s->worker(i); });
+  st = s;
+  return CDA_OK;
+}
+
+// Host memory that the DMA engines can read directly (hipHostMalloc'd or registered).
+static bool is_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not an error here
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+static bool direct(const cda_ctx* c, const void* host, size_t n, int dir_bit) {
+  return !(c->staging & dir_bit) || n < ((size_t)2 << 20) || is_pinned(host);
+}
+
+int staged_h2d(cda_ctx* c, void* d_dst, const void* h_src, size_t n, hipStream_t s) {
+  if (n == 0) return CDA_OK;
+  if (direct(c, h_src, n, 1))
+    return dev_ok(c, hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, s), "H2D") ? CDA_OK : CDA_E_DEVICE;
+  int rc = get_stager(c, c->st_in);
+  if (rc) return rc;
+  Stager& st = *c->st_in;
+  const size_t B = Stager::kSlotBytes;
+  for (size_t off = 0, i = 0; off < n; off += B, i++) {
+    const int j = (int)(i % Stager::kSlots);
+    const size_t len = std::min(B, n - off);
+    uint8_t* slot = st.ring + (size_t)j * B;
+    // the slot's previous DMA (chunk i - kSlots, or the last call's) has read it
+    if (st.used[j] && !dev_ok(c, hipEventSynchronize(st.ev[j]), "staging wait")) return CDA_E_DEVICE;
+    st.pmemcpy(slot, (const uint8_t*)h_src + off, len);
+    if (!dev_ok(c, hipMemcpyAsync((uint8_t*)d_dst + off, slot, len, hipMemcpyHostToDevice, s), "H2D") ||
+        !dev_ok(c, hipEventRecord(st.ev[j], s), "staging record"))
+      return CDA_E_DEVICE;
+    st.used[j] = true;
+  }
+  return CDA_OK;
+}
+
+int staged_d2h(cda_ctx* c, void* h_dst, const void* d_src, size_t n, hipStream_t s) {
+  if (n == 0) return CDA_OK;
+  if (direct(c, h_dst, n, 2))
+    return dev_ok(c, hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, s), "D2H") &&
+                   dev_ok(c, hipStreamSynchronize(s), "sync")
+               ? CDA_OK
+               : CDA_E_DEVICE;
+  int rc = get_stager(c, c->st_out);
+  if (rc) return rc;
+  Stager& st = *c->st_out;
+  const size_t B = Stager::kSlotBytes, nchunks = (n + B - 1) / B;
+  auto issue = [&](size_t i) {
+    const int j = (int)(i % Stager::kSlots);
+    const size_t off = i * B, len = std::min(B, n - off);
+    st.used[j] = true;
+    return dev_ok(c, hipMemcpyAsync(st.ring + (size_t)j * B, (const uint8_t*)d_src + off, len, hipMemcpyDeviceToHost,
+                                    s),
+                  "D2H") &&
+           dev_ok(c, hipEventRecord(st.ev[j], s), "staging record");
+  };
+  for (size_t i = 0; i < std::min<size_t>(Stager::kSlots, nchunks); i++)
+    if (!issue(i)) return CDA_E_DEVICE;
+  for (size_t i = 0; i < nchunks; i++) {
+    const int j = (int)(i % Stager::kSlots);
+    const size_t off = i * B, len = std::min(B, n - off);
+    if (!dev_ok(c, hipEventSynchronize(st.ev[j]), "staging wait")) return CDA_E_DEVICE;
+    st.pmemcpy((uint8_t*)h_dst + off, st.ring + (size_t)j * B, len);
+    if (i + Stager::kSlots < nchunks && !issue(i + Stager::kSlots)) return CDA_E_DEVICE;
+  }
+  return CDA_OK;
+}
+
+void free_staging(cda_ctx* c) {
+  delete c->st_in;
+  delete c->st_out;
+  c->st_in = c->st_out = nullptr;
+}
+
+}  // namespace cda
