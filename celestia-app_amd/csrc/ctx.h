@@ -36,7 +36,11 @@ struct cda_ctx {
   bool repair_fused_verify = true;
   // CDA_REPAIR_EARLY=0: repair copies the square back only at the end (no early row return)
   bool repair_early = true;
-  hipStream_t sub[kMaxSub] = {};
+  hipStream_t sub[kMaxSub] = {};  // created on first use (ensure_sub): experiment paths only
+  bool sub_ready = false;
+  // HIP maps streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues, so the streams that must run
+  // concurrently are created first, together: stream, h2d_stream, d2h_stream, aux_stream.
+  hipStream_t aux_stream = nullptr;
   // Workspace ordering across streams: the device-resident entry points enqueue on the caller's
   // stream but use this ctx's workspace (leaf/scratch records).  ws_event marks the end of the
   // last such enqueue; synchronous entry points make `stream` wait on it, and device entry points
@@ -95,6 +99,8 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
 // host-buffer batch as an H2D / compute / D2H pipeline (host_pipeline.cpp); caller holds the lock
 int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
                     uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err, int block0);
+int ensure_pipeline(cda_ctx* c);  // copy streams + per-slot events (host_pipeline.cpp)
+int ensure_sub(cda_ctx* c);       // the CDA_STREAMS / CDA_PIPELINE sub-streams (engine.cpp)
 void free_pipeline(cda_ctx* c);
 // Caller-memory copies (staging.cpp): large pageable buffers through the pinned rings, pinned / small ones
 // directly.  staged_h2d returns once the source may be released (DMA enqueued on s); staged_d2h once the

@@ -225,6 +225,15 @@ int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t
 // profiling so per-kernel event timings do not overlap).  Measured on MI355X:
 // one stream is as fast or faster (each kernel already fills the GPU), and
 // CU-masked streams (RS on some CUs, SHA on the rest) were 2-5x slower.
+int ensure_sub(cda_ctx* c) {
+  if (c->sub_ready) return CDA_OK;
+  for (int i = 0; i < cda_ctx::kMaxSub; i++)
+    if (!c->sub[i] && !dev_ok(c, hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking), "hipStreamCreate"))
+      return CDA_E_DEVICE;
+  c->sub_ready = true;
+  return CDA_OK;
+}
+
 int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                      void* d_dah, unsigned long long* d_status, hipStream_t s) {
   const uint32_t w = 2 * k;
@@ -238,6 +247,7 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
     // stream sub[1] hashes chunk i as soon as its RS phase is done, so the memory-bound
     // RS of chunk i+1 overlaps the VALU-bound hashing of chunk i.
     const uint32_t C = std::min<uint32_t>((uint32_t)c->pipe_chunks, nblocks);
+    if ((rc = ensure_sub(c))) return rc;
     hipStream_t srs = c->sub[0], ssha = c->sub[1];
     if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
         !dev_ok(c, hipStreamWaitEvent(srs, c->fork_ev, 0), "hipStreamWaitEvent") ||
@@ -278,6 +288,7 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   }
   const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
   if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
+  if ((rc = ensure_sub(c))) return rc;
   if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
   uint32_t done = 0;
   for (int i = 0; i < nsub; i++) {
@@ -337,12 +348,15 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
   if (const char* e = getenv("CDA_STAGING")) c->staging = atoi(e) & 3;
-  bool ok = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
+  // the streams that overlap each other, created right after `stream` so that they land on distinct hardware
+  // queues (HIP assigns streams to its GPU_MAX_HW_QUEUES = 4 queues round-robin)
+  bool ok = ensure_pipeline(c) == CDA_OK &&
+            hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
-    ok = hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
+    ok = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     delete c;
     return CDA_E_DEVICE;
@@ -368,6 +382,7 @@ void cda_free(cda_ctx* c) {
     }
     free_pipeline(c);
     free_staging(c);
+    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
     if (c->sync_ev) (void)hipEventDestroy(c->sync_ev);
@@ -570,14 +585,35 @@ int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint
       (rc = ensure(c, c->dah, (size_t)nblocks * 32)) || (rc = ensure(c, c->status, (size_t)nblocks * 8)))
     return rc;
   if (!dev_ok(c, hipMemcpyAsync(c->ods.p, ods, ods_b, hipMemcpyHostToDevice, c->stream), "H2D")) return CDA_E_DEVICE;
-  rc = enqueue_pipeline(c, k, nblocks, (const uint8_t*)c->ods.p, (uint8_t*)c->eds.p, c->roots.p, c->dah.p,
-                        (unsigned long long*)c->status.p, c->stream);
-  if (rc) return rc;
+  // With the EDS wanted (da.ExtendShares returns it): the EDS is final once the extension has run, so its copy-out
+  // runs on the D2H stream beside the tree hashing instead of after it.  The hashing is enqueued first: the
+  // pageable copy holds this thread until it is done.
+  const bool overlap = eds_or_null && !c->prof && !c->fused && c->pipe_chunks <= 1 && c->chunk_blocks == 0 &&
+                       c->nsub <= 1;
+  if (overlap) {
+    const size_t cells = (size_t)nblocks * w * w;
+    if ((rc = ensure_pipeline(c)) || (rc = ensure(c, c->leaf, cells * CDA_REC_BYTES)) ||
+        (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)) ||
+        (rc = enqueue_rs(c, k, nblocks, (const uint8_t*)c->ods.p, (uint8_t*)c->eds.p, c->stream)))
+      return rc;
+    if (!dev_ok(c, hipEventRecord(c->ev_comp[0], c->stream), "hipEventRecord")) return CDA_E_DEVICE;
+    if ((rc = enqueue_commit(c, k, nblocks, (const uint8_t*)c->eds.p, c->roots.p, c->dah.p,
+                             (unsigned long long*)c->status.p, c->stream, 0)))
+      return rc;
+    if (!dev_ok(c, hipStreamWaitEvent(c->d2h_stream, c->ev_comp[0], 0), "hipStreamWaitEvent") ||
+        !dev_ok(c, hipMemcpyAsync(eds_or_null, c->eds.p, eds_b, hipMemcpyDeviceToHost, c->d2h_stream), "D2H") ||
+        !dev_ok(c, hipStreamSynchronize(c->d2h_stream), "sync"))
+      return CDA_E_DEVICE;
+  } else {
+    rc = enqueue_pipeline(c, k, nblocks, (const uint8_t*)c->ods.p, (uint8_t*)c->eds.p, c->roots.p, c->dah.p,
+                          (unsigned long long*)c->status.p, c->stream);
+    if (rc) return rc;
+    if (eds_or_null &&
+        !dev_ok(c, hipMemcpyAsync(eds_or_null, c->eds.p, eds_b, hipMemcpyDeviceToHost, c->stream), "D2H"))
+      return CDA_E_DEVICE;
+  }
   std::vector<uint8_t> recs(roots_b);
   std::vector<uint64_t> st(nblocks);
-  if (eds_or_null &&
-      !dev_ok(c, hipMemcpyAsync(eds_or_null, c->eds.p, eds_b, hipMemcpyDeviceToHost, c->stream), "D2H"))
-    return CDA_E_DEVICE;
   if (!dev_ok(c, hipMemcpyAsync(recs.data(), c->roots.p, roots_b, hipMemcpyDeviceToHost, c->stream), "D2H") ||
       !dev_ok(c, hipMemcpyAsync(dah, c->dah.p, (size_t)nblocks * 32, hipMemcpyDeviceToHost, c->stream), "D2H") ||
       !dev_ok(c, hipMemcpyAsync(st.data(), c->status.p, (size_t)nblocks * 8, hipMemcpyDeviceToHost, c->stream), "D2H") ||

@@ -370,16 +370,19 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   // Verification streams.  Decodes run in order on `s`; batch b's verification runs after decode b
   // on a second stream, overlapping decode b+1 (which writes only cells missing after batch b, and
   // every axis batch b verifies is complete after it).  The fused kernel keeps its trees in LDS, so
-  // batches verify concurrently on 3 streams; the generic path shares the leaf / level workspace.
-  const int nvs = c->repair_overlap ? (c->repair_fused_verify ? 3 : 1) : 0;
-  auto vstream = [&](size_t b) { return nvs ? c->sub[cda_ctx::kMaxSub - 1 - (int)(b % nvs)] : s; };
+  // batches verify concurrently on 2 streams; the generic path shares the leaf / level workspace.
+  // (aux_stream and h2d_stream sit on hardware queues of their own, see ctx.h; the rows going back
+  // early use d2h_stream.)
+  const int nvs = c->repair_overlap ? (c->repair_fused_verify ? 2 : 1) : 0;
+  hipStream_t vs[2] = {c->aux_stream, c->h2d_stream};
+  auto vstream = [&](size_t b) { return nvs ? vs[b % nvs] : s; };
   auto fork = [&](hipStream_t v) {
     return v == s || (dev_ok(c, hipEventRecord(c->fork_ev, s), "event") &&
                       dev_ok(c, hipStreamWaitEvent(v, c->fork_ev, 0), "wait"));
   };
   auto join = [&]() {
     for (int i = 0; i < nvs; i++)
-      if (!dev_ok(c, hipEventRecord(c->join_ev[i], c->sub[cda_ctx::kMaxSub - 1 - i]), "event") ||
+      if (!dev_ok(c, hipEventRecord(c->join_ev[i], vs[i]), "event") ||
           !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[i], 0), "wait"))
         return false;
     return true;
@@ -475,7 +478,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   if (early)  // rows whose last writer has run go back on their own stream (pageable: from a helper thread)
     early_d2h = std::thread([&] {
       (void)hipSetDevice(c->device);
-      hipStream_t d2h = c->sub[cda_ctx::kMaxSub - 4];
+      hipStream_t d2h = c->d2h_stream;
       const size_t row_b = W * CDA_SHARE;
       for (size_t b = 0; b < nbat && !early_failed; b++) {
         if (!bev[b]) continue;
