@@ -248,7 +248,7 @@ struct Rs8RegArgs {
 //   P1 f=1: IFFT d=0 (cross-lane), d=1..3 | exchange | P2 f=L-3: IFFT d=4..L-1,
 //   FFT d=L-1..L-3 | exchange | P3 f=1: FFT d=min(3,L-4)..1, d=0 (cross-lane).
 // ===========================================================================
-__device__ __forceinline__ int x2_of(int w, int sw, int r, int f) {
+__host__ __device__ constexpr int x2_of(int w, int sw, int r, int f) {
   // bits 1..L-1 of the element index: 3 register bits at (f..f+2), wave bits elsewhere
   const int y = ((w >> (f - 1)) << (f + 2)) | (r << (f - 1)) | (w & ((1 << (f - 1)) - 1));
   return (y << 1) | sw;
@@ -345,6 +345,101 @@ __device__ __forceinline__ void layer2_d0(uint32_t (&E)[8][8], int w, int f, boo
   }
 }
 
+// ---- P1 / P3 with compile-time constants ------------------------------------
+// In the f = 1 layout the constants of layers d = 0..3 are functions of the register bits and of the wave
+// index w (bits 4..L-1).  w is wave-uniform, so a scalar branch on it selects a copy of P1 / P3 specialised for
+// that wave, where every constant is again a compile-time value (the GF(2)-matrix multiply of gf8_const.h,
+// ~18 VALU) instead of the runtime form (gf8_mul_asm.h, ~45 VALU + scalar branches).  Costs code size:
+// 2^(L-4) copies of P1 and P3.
+#ifndef CDA_RS_WCONST
+#define CDA_RS_WCONST 1
+#endif
+
+template <bool INVERSE, unsigned C>
+__device__ __forceinline__ void bfly_cc(uint32_t (&X)[8], uint32_t (&Y)[8]) {
+  if (INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+  }
+  if constexpr (C != 0u) gf8_muladd_const<C>(X, Y);
+  if (!INVERSE) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
+  }
+}
+
+// layer d >= 1 of the f = 1 layout (register bit d - 1), wave W
+template <bool INVERSE, int M, int W, int D, int R>
+__device__ __forceinline__ void bfly_w(uint32_t (&E)[8][8]) {
+  constexpr int rb = D - 1;
+  if constexpr (!(R & (1 << rb))) {
+    constexpr int x = x2_of(W, 0, R, 1);
+    constexpr int s0 = (x >> (D + 1)) << (D + 1);
+    constexpr int idx = INVERSE ? (M - 1 + s0 + (1 << D)) : (s0 + (1 << D) - 1);
+    bfly_cc<INVERSE, kCpoly8.v[idx]>(E[R], E[R | (1 << rb)]);
+  }
+}
+
+template <bool INVERSE, int M, int W, int D>
+__device__ __forceinline__ void layer_w(uint32_t (&E)[8][8]) {
+  bfly_w<INVERSE, M, W, D, 0>(E);
+  bfly_w<INVERSE, M, W, D, 1>(E);
+  bfly_w<INVERSE, M, W, D, 2>(E);
+  bfly_w<INVERSE, M, W, D, 3>(E);
+  bfly_w<INVERSE, M, W, D, 4>(E);
+  bfly_w<INVERSE, M, W, D, 5>(E);
+  bfly_w<INVERSE, M, W, D, 6>(E);
+  bfly_w<INVERSE, M, W, D, 7>(E);
+}
+
+// layer d = 0 across the lane halves (as layer2_d0), wave W
+template <bool INVERSE, int M, int W, int R>
+__device__ __forceinline__ void d0_w(uint32_t (&E)[8][8]) {
+  constexpr int x = x2_of(W, 0, R, 1);
+  uint32_t X[8], Y[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const auto p = __builtin_amdgcn_permlane32_swap(E[R][j], E[R][j], false, false);
+    X[j] = p[0];
+    Y[j] = p[1];
+  }
+  bfly_cc<INVERSE, kCpoly8.v[INVERSE ? (M - 1 + x + 1) : x]>(X, Y);
+#pragma unroll
+  for (int j = 0; j < 8; j++) E[R][j] = __builtin_amdgcn_permlane32_swap(X[j], Y[j], false, false)[0];
+  __builtin_amdgcn_sched_barrier(0);  // one butterfly's temporaries live at a time
+}
+
+template <bool INVERSE, int M, int W>
+__device__ __forceinline__ void layer_d0_w(uint32_t (&E)[8][8]) {
+  d0_w<INVERSE, M, W, 0>(E);
+  d0_w<INVERSE, M, W, 1>(E);
+  d0_w<INVERSE, M, W, 2>(E);
+  d0_w<INVERSE, M, W, 3>(E);
+  d0_w<INVERSE, M, W, 4>(E);
+  d0_w<INVERSE, M, W, 5>(E);
+  d0_w<INVERSE, M, W, 6>(E);
+  d0_w<INVERSE, M, W, 7>(E);
+}
+
+// P1: IFFT d = 0..min(3, L-1); P3: FFT d = min(F2-1, 3)..1, then d = 0
+template <int L, int W>
+__device__ __forceinline__ void p1_w(uint32_t (&E)[8][8]) {
+  constexpr int M = 1 << L;
+  layer_d0_w<true, M, W>(E);
+  layer_w<true, M, W, 1>(E);
+  if constexpr (L > 2) layer_w<true, M, W, 2>(E);
+  if constexpr (L > 3) layer_w<true, M, W, 3>(E);
+}
+
+template <int L, int W>
+__device__ __forceinline__ void p3_w(uint32_t (&E)[8][8]) {
+  constexpr int M = 1 << L, F2 = L - 3;
+  if constexpr (F2 - 1 >= 3) layer_w<false, M, W, 3>(E);
+  if constexpr (F2 - 1 >= 2) layer_w<false, M, W, 2>(E);
+  if constexpr (F2 - 1 >= 1) layer_w<false, M, W, 1>(E);
+  layer_d0_w<false, M, W>(E);
+}
+
 // LDS exchange of the 8 x 8 register state between layouts (two halves of 4 planes).
 template <int M>
 __device__ __forceinline__ void exchange2(uint32_t (&E)[8][8], uint4* xbuf, int w, int sw, int li, int f_from,
@@ -371,12 +466,11 @@ __device__ __forceinline__ void exchange2(uint32_t (&E)[8][8], uint4* xbuf, int 
 }
 
 // Work of workgroup `wg` (blockDim = 64 << (L - 4)); xbuf = [M][32] x 16 B LDS (L > 4).
-template <int L>
-__device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* xbuf) {
+// WC >= 0: the body of wave w == WC with P1 / P3 specialised for it; WC < 0: runtime constants.
+template <int L, int WC>
+__device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* xbuf, int w) {
   constexpr int M = 1 << L;
-  constexpr int NW = 1 << (L - 4);
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & (NW - 1);
   const int u = lane & 15, cwi = (lane >> 4) & 1, sw = lane >> 5, li = lane & 31;
   const bool upper = sw != 0;
   const int slice = wg % a.slices;
@@ -416,17 +510,25 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
   }
   constexpr int F2 = L - 3;  // P2 register bits F2..F2+2 = L-3..L-1
   // P1 (f=1): IFFT d=0 (cross-lane), d=1..3 (or up to L-1 when L == 4)
-  layer2_d0<true, M>(E, w, 1, upper);
+  if constexpr (WC >= 0) {
+    p1_w<L, WC>(E);
+  } else {
+    layer2_d0<true, M>(E, w, 1, upper);
 #pragma unroll
-  for (int d = 1; d < 4 && d < L; d++) layer2_u<true, M>(E, w, 1, d);
+    for (int d = 1; d < 4 && d < L; d++) layer2_u<true, M>(E, w, 1, d);
+  }
   if (L > 4) exchange2<M>(E, xbuf, w, sw, li, 1, F2);
   // P2: IFFT d=4..L-1, FFT d=L-1..F2 (compile-time constants)
   p2_layers<L, (F2 > 1 ? F2 : 1), 4, true>(E);
   if (L > 4) exchange2<M>(E, xbuf, w, sw, li, F2, 1);
   // P3 (f=1): FFT d=F2-1..1, then d=0 (cross-lane)
+  if constexpr (WC >= 0) {
+    p3_w<L, WC>(E);
+  } else {
 #pragma unroll
-  for (int d = (F2 - 1 < 3 ? F2 - 1 : 3); d >= 1; d--) layer2_u<false, M>(E, w, 1, d);
-  layer2_d0<false, M>(E, w, 1, upper);
+    for (int d = (F2 - 1 < 3 ? F2 - 1 : 3); d >= 1; d--) layer2_u<false, M>(E, w, 1, d);
+    layer2_d0<false, M>(E, w, 1, upper);
+  }
   const SliceMasks ko = slice_masks();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
@@ -442,6 +544,28 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
       q[16] = make_uint4(v[4], v[5], v[6], v[7]);
     }
   }
+}
+
+// scalar dispatch on the wave index (w is an SGPR value): one whole body per wave index, so that no
+// control-flow merge with the 64 live state registers follows the specialised phases (a merge after
+// P1 or P3 alone made the register allocator spill)
+template <int L, int W>
+__device__ __forceinline__ void rs_g2_select(const Rs8RegArgs& a, int wg, uint4* xbuf, int w) {
+  if constexpr (W < (1 << (L - 4))) {
+    if (w == W)
+      rs_g2_impl<L, W>(a, wg, xbuf, w);
+    else
+      rs_g2_select<L, W + 1>(a, wg, xbuf, w);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* xbuf) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & ((1 << (L - 4)) - 1);
+  if constexpr (CDA_RS_WCONST)
+    rs_g2_select<L, 0>(a, wg, xbuf, w);
+  else
+    rs_g2_impl<L, -1>(a, wg, xbuf, w);
 }
 
 template <int L>
