@@ -123,4 +123,133 @@ __device__ __forceinline__ void gf8_muladd_const(uint32_t (&X)[8], const uint32_
   gf8_row_add<gf8_row(C, 7)>(X[7], Y);
 }
 
+// ---- multiply in Leopard's own (Cantor) coordinates, with shared XOR terms ------------------------------------
+// Once every constant of the encoder is a compile-time value (rs_kernels.hip, P1/P2/P3), the basis only matters
+// through the density of the constants' matrices, and the Cantor basis (the byte bits themselves) is as dense as the
+// standard one for the FF8 constants (within 2 %), so the planes stay in Leopard's coordinates and the two basis
+// changes per element disappear.  Leopard's x*exp(L) is phi^-1(alpha^L * phi(x)); column j of its matrix is
+// phi^-1(c * phi(e_j)) with c = alpha^L in the standard basis (the kCpoly8 entry).
+constexpr unsigned gf8_mulstd(unsigned a, unsigned b) {
+  unsigned r = 0;
+  while (b) {
+    if (b & 1u) r ^= a;
+    a <<= 1;
+    if (a & 0x100u) a ^= 0x11Du;
+    b >>= 1;
+  }
+  return r;
+}
+constexpr unsigned kPhi8[8] = {1, 214, 152, 146, 86, 200, 88, 230};
+constexpr unsigned kPhiInv8[8] = {1, 104, 92, 100, 114, 240, 86, 18};
+constexpr unsigned gf8_apply(const unsigned (&cols)[8], unsigned v) {
+  unsigned r = 0;
+  for (int j = 0; j < 8; j++)
+    if ((v >> j) & 1u) r ^= cols[j];
+  return r;
+}
+// row i of x -> phi^-1(c * phi(x)): bit j set when bit i of column j is set
+constexpr unsigned gf8_row_cantor(unsigned c, int i) {
+  unsigned row = 0;
+  for (int j = 0; j < 8; j++) {
+    const unsigned col = gf8_apply(kPhiInv8, gf8_mulstd(c, kPhi8[j]));
+    row |= ((col >> i) & 1u) << j;
+  }
+  return row;
+}
+
+// X[i] ^= XOR of Y[j] over row i, as a straight-line program of 3-input XORs.  Greedy common-subexpression pass:
+// while some triple of terms appears in >= 2 rows (or a pair in >= 3), one v_bitop3 makes it a temporary that those
+// rows use instead (~17 % fewer VALU than row by row over the constants of a k = 128 encode).
+struct Gf8Prog {
+  int n;            // number of ops
+  int dst[48];      // >= 0: X[dst] ^= ...; < 0: temporary value index -dst (>= 8)
+  int s[48][3];     // source value indices (0..7 = Y planes, >= 8 temporaries), -1 = unused
+};
+constexpr Gf8Prog gf8_prog(unsigned c) {
+  Gf8Prog p{};
+  unsigned rows[8] = {};
+  for (int i = 0; i < 8; i++) rows[i] = gf8_row_cantor(c, i);
+  int nv = 8;
+  for (;;) {
+    int best_g = 0, bs[3] = {-1, -1, -1};
+    for (int a = 0; a < nv; a++)
+      for (int b = a + 1; b < nv; b++) {
+        const unsigned mab = (1u << a) | (1u << b);
+        int n2 = 0;
+        for (int i = 0; i < 8; i++) n2 += (rows[i] & mab) == mab;
+        if (n2 - 2 > best_g) {  // doubled gains: pair n*0.5-1, triple n-1
+          best_g = n2 - 2;
+          bs[0] = a, bs[1] = b, bs[2] = -1;
+        }
+        for (int d = b + 1; d < nv; d++) {
+          const unsigned m3 = mab | (1u << d);
+          int n3 = 0;
+          for (int i = 0; i < 8; i++) n3 += (rows[i] & m3) == m3;
+          if (2 * n3 - 2 > best_g) {
+            best_g = 2 * n3 - 2;
+            bs[0] = a, bs[1] = b, bs[2] = d;
+          }
+        }
+      }
+    if (best_g <= 0 || nv >= 24) break;
+    unsigned m = (1u << bs[0]) | (1u << bs[1]) | (bs[2] >= 0 ? 1u << bs[2] : 0u);
+    p.dst[p.n] = -nv;
+    p.s[p.n][0] = bs[0], p.s[p.n][1] = bs[1], p.s[p.n][2] = bs[2];
+    p.n++;
+    for (int i = 0; i < 8; i++)
+      if ((rows[i] & m) == m) rows[i] = (rows[i] & ~m) | (1u << nv);
+    nv++;
+  }
+  for (int i = 0; i < 8; i++) {
+    unsigned r = rows[i];
+    while (r) {
+      const int a = ctz8(r);
+      r &= r - 1;
+      int b = -1;
+      if (r) {
+        b = ctz8(r);
+        r &= r - 1;
+      }
+      p.dst[p.n] = i;
+      p.s[p.n][0] = a, p.s[p.n][1] = b, p.s[p.n][2] = -1;
+      p.n++;
+    }
+  }
+  return p;
+}
+
+template <unsigned C>
+struct Gf8ProgOf {
+  static constexpr Gf8Prog p = gf8_prog(C);
+};
+
+template <unsigned C, int I>
+__device__ __forceinline__ void gf8_prog_run(uint32_t (&X)[8], uint32_t (&V)[24]) {
+  if constexpr (I < Gf8ProgOf<C>::p.n) {
+    constexpr int d = Gf8ProgOf<C>::p.dst[I];
+    constexpr int a = Gf8ProgOf<C>::p.s[I][0], b = Gf8ProgOf<C>::p.s[I][1], e = Gf8ProgOf<C>::p.s[I][2];
+    if constexpr (d < 0) {
+      if constexpr (e >= 0)
+        V[-d] = xor3c(V[a], V[b], V[e]);
+      else
+        V[-d] = V[a] ^ V[b];
+    } else {
+      if constexpr (b >= 0)
+        X[d] = xor3c(X[d], V[a], V[b]);
+      else
+        X[d] ^= V[a];
+    }
+    gf8_prog_run<C, I + 1>(X, V);
+  }
+}
+
+// X ^= c * Y on 8 bit-planes in Leopard's coordinates, c = alpha^L (standard basis) a compile-time constant
+template <unsigned C>
+__device__ __forceinline__ void gf8_muladd_cantor(uint32_t (&X)[8], const uint32_t (&Y)[8]) {
+  uint32_t V[24];
+#pragma unroll
+  for (int j = 0; j < 8; j++) V[j] = Y[j];
+  gf8_prog_run<C, 0>(X, V);
+}
+
 }  // namespace cda

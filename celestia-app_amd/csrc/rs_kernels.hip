@@ -267,6 +267,23 @@ __device__ __forceinline__ void layer2_u(uint32_t (&E)[8][8], int w, int f, int 
   }
 }
 
+#ifndef CDA_RS_WCONST
+#define CDA_RS_WCONST 1
+#endif
+// CDA_RS_CANTOR: planes in Leopard's own coordinates (no basis change at load / store), every multiply a
+// compile-time matrix program (gf8_const.h gf8_muladd_cantor); needs the specialised P1 / P3 (CDA_RS_WCONST).
+#ifndef CDA_RS_CANTOR
+#define CDA_RS_CANTOR CDA_RS_WCONST
+#endif
+static_assert(!CDA_RS_CANTOR || CDA_RS_WCONST, "the Cantor-coordinate encoder has no runtime-constant multiply");
+template <unsigned C>
+__device__ __forceinline__ void gf8_muladd_k(uint32_t (&X)[8], const uint32_t (&Y)[8]) {
+  if constexpr (CDA_RS_CANTOR)
+    gf8_muladd_cantor<C>(X, Y);
+  else
+    gf8_muladd_const<C>(X, Y);
+}
+
 // P2 layers (register bits F..F+2 = the top three index bits, d >= F): every index bit above d is a register
 // bit, so the constant of each butterfly is a compile-time value and the multiply is its GF(2) matrix
 // (gf8_const.h) -- no scalar branches, about 18 VALU instead of ~45.
@@ -284,7 +301,7 @@ __device__ __forceinline__ void bfly_const(uint32_t (&E)[8][8]) {
 #pragma unroll
       for (int j = 0; j < 8; j++) Y[j] ^= X[j];
     }
-    if constexpr (c != 0u) gf8_muladd_const<c>(X, Y);
+    if constexpr (c != 0u) gf8_muladd_k<c>(X, Y);
     if (!INVERSE) {
 #pragma unroll
       for (int j = 0; j < 8; j++) Y[j] ^= X[j];
@@ -351,17 +368,13 @@ __device__ __forceinline__ void layer2_d0(uint32_t (&E)[8][8], int w, int f, boo
 // that wave, where every constant is again a compile-time value (the GF(2)-matrix multiply of gf8_const.h,
 // ~18 VALU) instead of the runtime form (gf8_mul_asm.h, ~45 VALU + scalar branches).  Costs code size:
 // 2^(L-4) copies of P1 and P3.
-#ifndef CDA_RS_WCONST
-#define CDA_RS_WCONST 1
-#endif
-
 template <bool INVERSE, unsigned C>
 __device__ __forceinline__ void bfly_cc(uint32_t (&X)[8], uint32_t (&Y)[8]) {
   if (INVERSE) {
 #pragma unroll
     for (int j = 0; j < 8; j++) Y[j] ^= X[j];
   }
-  if constexpr (C != 0u) gf8_muladd_const<C>(X, Y);
+  if constexpr (C != 0u) gf8_muladd_k<C>(X, Y);
   if (!INVERSE) {
 #pragma unroll
     for (int j = 0; j < 8; j++) Y[j] ^= X[j];
@@ -377,6 +390,7 @@ __device__ __forceinline__ void bfly_w(uint32_t (&E)[8][8]) {
     constexpr int s0 = (x >> (D + 1)) << (D + 1);
     constexpr int idx = INVERSE ? (M - 1 + s0 + (1 << D)) : (s0 + (1 << D) - 1);
     bfly_cc<INVERSE, kCpoly8.v[idx]>(E[R], E[R | (1 << rb)]);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -392,52 +406,108 @@ __device__ __forceinline__ void layer_w(uint32_t (&E)[8][8]) {
   bfly_w<INVERSE, M, W, D, 7>(E);
 }
 
-// layer d = 0 across the lane halves (as layer2_d0), wave W
+// layer d = 0, wave W.  With the specialised phases the element index bit 0 sits on lane bit 0 (CDA_RS_DPP), so a
+// butterfly's two elements are in lanes 2i and 2i+1 and one DPP quad_perm read hands each lane its partner's plane,
+// folded into the XOR.  Each lane computes only its own output; `lm` is all-ones in the x (even) lanes:
+//   IFFT: T = x ^ y;  x' = x ^ c*T, y' = T                      (c*T computed wave-wide, kept in x lanes)
+//   FFT:  S = y (own or partner), T = x ^ y;  x' = x ^ c*S, y' = T ^ c*S = (lm ? x : T) ^ c*S
+// Without CDA_RS_DPP (lane bit 5): v_permlane32_swap hands both halves both elements, both compute the butterfly.
+#ifndef CDA_RS_DPP
+#define CDA_RS_DPP CDA_RS_WCONST
+#endif
+__device__ __forceinline__ uint32_t lane_pair_xor(uint32_t v) {  // v ^ v[lane ^ 1]
+  return v ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+}
+// T[j] = E[j] ^ E[j][lane ^ 1] for 8 planes as one volatile block: with the intrinsic the compiler hoisted the DPP
+// reads of all eight FFT d = 0 butterflies ahead of the first (64 extra live VGPRs, spills).  s_nop 1 covers the
+// VALU-write -> DPP-read hazard (2 wait states) for inputs written just before the block.
+__device__ __forceinline__ void lane_pair_xor8(uint32_t (&T)[8], const uint32_t (&E)[8]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_xor_b32_dpp %0, %8, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %1, %9, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %2, %10, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %3, %11, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %4, %12, %12 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %5, %13, %13 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %6, %14, %14 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_xor_b32_dpp %7, %15, %15 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "=&v"(T[0]), "=&v"(T[1]), "=&v"(T[2]), "=&v"(T[3]), "=&v"(T[4]), "=&v"(T[5]), "=&v"(T[6]), "=&v"(T[7])
+      : "v"(E[0]), "v"(E[1]), "v"(E[2]), "v"(E[3]), "v"(E[4]), "v"(E[5]), "v"(E[6]), "v"(E[7]));
+}
 template <bool INVERSE, int M, int W, int R>
-__device__ __forceinline__ void d0_w(uint32_t (&E)[8][8]) {
+__device__ __forceinline__ void d0_w(uint32_t (&E)[8][8], uint32_t lm) {
   constexpr int x = x2_of(W, 0, R, 1);
-  uint32_t X[8], Y[8];
+  constexpr unsigned c = kCpoly8.v[INVERSE ? (M - 1 + x + 1) : x];
+  if constexpr (CDA_RS_DPP) {
+    uint32_t T[8];
+    if constexpr (INVERSE) {
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
-    const auto p = __builtin_amdgcn_permlane32_swap(E[R][j], E[R][j], false, false);
-    X[j] = p[0];
-    Y[j] = p[1];
+      for (int j = 0; j < 8; j++) T[j] = lane_pair_xor(E[R][j]);
+    } else {
+      lane_pair_xor8(T, E[R]);
+    }
+    if constexpr (INVERSE) {
+      if constexpr (c != 0u) gf8_muladd_k<c>(E[R], T);
+#pragma unroll
+      for (int j = 0; j < 8; j++) E[R][j] = __builtin_amdgcn_bitop3_b32(lm, E[R][j], T[j], 0xCA);  // lm ? E : T
+    } else {
+      uint32_t S[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        S[j] = __builtin_amdgcn_bitop3_b32(E[R][j], T[j], lm, 0x78);       // E ^ (T & lm) = y
+        E[R][j] = __builtin_amdgcn_bitop3_b32(lm, E[R][j], T[j], 0xCA);    // lm ? x : T
+      }
+      if constexpr (c != 0u) gf8_muladd_k<c>(E[R], S);
+    }
+    // pin the results here: otherwise the compiler sinks this arithmetic into the (conditional) store blocks
+    // while the DPP reads stay put, and every butterfly's T / S stays live until the stores
+#pragma unroll
+    for (int j = 0; j < 8; j++) asm volatile("" : "+v"(E[R][j]));
+  } else {
+    uint32_t X[8], Y[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const auto p = __builtin_amdgcn_permlane32_swap(E[R][j], E[R][j], false, false);
+      X[j] = p[0];
+      Y[j] = p[1];
+    }
+    bfly_cc<INVERSE, c>(X, Y);
+#pragma unroll
+    for (int j = 0; j < 8; j++) E[R][j] = __builtin_amdgcn_permlane32_swap(X[j], Y[j], false, false)[0];
   }
-  bfly_cc<INVERSE, kCpoly8.v[INVERSE ? (M - 1 + x + 1) : x]>(X, Y);
-#pragma unroll
-  for (int j = 0; j < 8; j++) E[R][j] = __builtin_amdgcn_permlane32_swap(X[j], Y[j], false, false)[0];
   __builtin_amdgcn_sched_barrier(0);  // one butterfly's temporaries live at a time
 }
 
 template <bool INVERSE, int M, int W>
-__device__ __forceinline__ void layer_d0_w(uint32_t (&E)[8][8]) {
-  d0_w<INVERSE, M, W, 0>(E);
-  d0_w<INVERSE, M, W, 1>(E);
-  d0_w<INVERSE, M, W, 2>(E);
-  d0_w<INVERSE, M, W, 3>(E);
-  d0_w<INVERSE, M, W, 4>(E);
-  d0_w<INVERSE, M, W, 5>(E);
-  d0_w<INVERSE, M, W, 6>(E);
-  d0_w<INVERSE, M, W, 7>(E);
+__device__ __forceinline__ void layer_d0_w(uint32_t (&E)[8][8], uint32_t lm) {
+  d0_w<INVERSE, M, W, 0>(E, lm);
+  d0_w<INVERSE, M, W, 1>(E, lm);
+  d0_w<INVERSE, M, W, 2>(E, lm);
+  d0_w<INVERSE, M, W, 3>(E, lm);
+  d0_w<INVERSE, M, W, 4>(E, lm);
+  d0_w<INVERSE, M, W, 5>(E, lm);
+  d0_w<INVERSE, M, W, 6>(E, lm);
+  d0_w<INVERSE, M, W, 7>(E, lm);
 }
 
 // P1: IFFT d = 0..min(3, L-1); P3: FFT d = min(F2-1, 3)..1, then d = 0
 template <int L, int W>
-__device__ __forceinline__ void p1_w(uint32_t (&E)[8][8]) {
+__device__ __forceinline__ void p1_w(uint32_t (&E)[8][8], uint32_t lm) {
   constexpr int M = 1 << L;
-  layer_d0_w<true, M, W>(E);
+  layer_d0_w<true, M, W>(E, lm);
   layer_w<true, M, W, 1>(E);
   if constexpr (L > 2) layer_w<true, M, W, 2>(E);
   if constexpr (L > 3) layer_w<true, M, W, 3>(E);
 }
 
 template <int L, int W>
-__device__ __forceinline__ void p3_w(uint32_t (&E)[8][8]) {
+__device__ __forceinline__ void p3_w(uint32_t (&E)[8][8], uint32_t lm) {
   constexpr int M = 1 << L, F2 = L - 3;
   if constexpr (F2 - 1 >= 3) layer_w<false, M, W, 3>(E);
   if constexpr (F2 - 1 >= 2) layer_w<false, M, W, 2>(E);
   if constexpr (F2 - 1 >= 1) layer_w<false, M, W, 1>(E);
-  layer_d0_w<false, M, W>(E);
+  layer_d0_w<false, M, W>(E, lm);
 }
 
 // LDS exchange of the 8 x 8 register state between layouts (two halves of 4 planes).
@@ -471,8 +541,14 @@ template <int L, int WC>
 __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* xbuf, int w) {
   constexpr int M = 1 << L;
   const int lane = threadIdx.x & 63;
-  const int u = lane & 15, cwi = (lane >> 4) & 1, sw = lane >> 5, li = lane & 31;
+  // lane = (li, sw): sw = element index bit 0 on lane bit 0 (DPP pairs) or lane bit 5 (permlane32 halves);
+  // li = unit u (16) and codeword cwi (2)
+  constexpr int SWB = (CDA_RS_DPP && WC >= 0) ? 0 : 5;
+  const int sw = (lane >> SWB) & 1, li = SWB == 0 ? lane >> 1 : lane & 31;
+  const int u = li & 15, cwi = li >> 4;
   const bool upper = sw != 0;
+  uint32_t lm = sw ? 0u : ~0u;  // x lanes of the d = 0 butterflies
+  asm volatile("" : "+v"(lm));
   const int slice = wg % a.slices;
   wg /= a.slices;
   const int grp = wg % a.groups_per_blk;
@@ -488,10 +564,13 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
 
   uint32_t E[8][8];
   const SliceMasks km = slice_masks();
+  const int wv = WC >= 0 ? WC : w;
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    const int x = x2_of(w, sw, r, 1);
-    if (x < a.k) {
+    // x0 (the pair's even element) is wave-uniform and, k being even on this path, x < k iff x0 < k: the branch is
+    // scalar, so no lane-divergent control flow surrounds the cross-lane butterflies
+    const int x = x2_of(wv, sw, r, 1), x0 = x2_of(wv, 0, r, 1);
+    if (x0 < a.k) {
       const uint4* p = reinterpret_cast<const uint4*>(src + x * a.src_sh);
       const uint4 v0 = p[0], v1 = p[16];
       if (cpy) {
@@ -502,7 +581,7 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
       E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
       E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
       bitslice8(E[r], km);
-      to_std8(E[r]);  // Cantor coordinates -> standard basis
+      if constexpr (!CDA_RS_CANTOR) to_std8(E[r]);  // Cantor coordinates -> standard basis
     } else {
 #pragma unroll
       for (int j = 0; j < 8; j++) E[r][j] = 0;
@@ -511,7 +590,7 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
   constexpr int F2 = L - 3;  // P2 register bits F2..F2+2 = L-3..L-1
   // P1 (f=1): IFFT d=0 (cross-lane), d=1..3 (or up to L-1 when L == 4)
   if constexpr (WC >= 0) {
-    p1_w<L, WC>(E);
+    p1_w<L, WC>(E, lm);
   } else {
     layer2_d0<true, M>(E, w, 1, upper);
 #pragma unroll
@@ -523,7 +602,7 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
   if (L > 4) exchange2<M>(E, xbuf, w, sw, li, F2, 1);
   // P3 (f=1): FFT d=F2-1..1, then d=0 (cross-lane)
   if constexpr (WC >= 0) {
-    p3_w<L, WC>(E);
+    p3_w<L, WC>(E, lm);
   } else {
 #pragma unroll
     for (int d = (F2 - 1 < 3 ? F2 - 1 : 3); d >= 1; d--) layer2_u<false, M>(E, w, 1, d);
@@ -532,12 +611,12 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
   const SliceMasks ko = slice_masks();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    const int x = x2_of(w, sw, r, 1);
-    if (x < a.k) {
+    const int x = x2_of(wv, sw, r, 1), x0 = x2_of(wv, 0, r, 1);
+    if (x0 < a.k) {  // wave-uniform, as at the load
       uint32_t v[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) v[j] = E[r][j];
-      to_cantor8(v);  // standard basis -> Cantor coordinates
+      if constexpr (!CDA_RS_CANTOR) to_cantor8(v);  // standard basis -> Cantor coordinates
       bitslice8(v, ko);
       uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
       q[0] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -781,7 +860,7 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   if (j.k < 1 || j.k > 128 || j.shard_len % 64 != 0) return -2;
   const int L = ilog2(j.k);
   // Batched path: 2 codewords per workgroup, register-resident (k >= 16).
-  if (L >= 4 && j.cw_per_blk % 2 == 0 && j.shard_len % 512 == 0) {
+  if (L >= 4 && j.k % 2 == 0 && j.cw_per_blk % 2 == 0 && j.shard_len % 512 == 0) {
     const Rs8RegArgs r = reg_args(j);
     const long long grid = (long long)j.nblk * r.groups_per_blk * r.slices;
     if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
