@@ -14,9 +14,11 @@
 // 32 bytes a lane owns are bit-sliced into 8 plane words (bit j of 32 bytes per
 // word) and butterflies are whole-register XORs.  Two kernels:
 //  * rs_encode8_g2_kernel (batched EDS path): 2 codewords per workgroup held in
-//    registers, lane index bit 0 of the element index, wave-uniform constants,
-//    multiply in the standard polynomial basis (x^8+x^4+x^3+x^2+1) by uniform
-//    branches over the constant's bits -- full-rate v_xor only.
+//    registers, lane bit 0 = element index bit 0 (d = 0 butterflies over DPP lane
+//    pairs), every other index bit a register or wave bit.  One body per wave
+//    index, so every layer constant is a compile-time value and each multiply is a
+//    fixed XOR3 program on the planes in Leopard's own (Cantor) coordinates
+//    (gf8_const.h) -- full-rate v_xor / v_bitop3 only, no scalar branches.
 //  * rs_encode8_kernel (single codewords / small k / odd shard lengths): state
 //    in LDS, radix-2 layers, constant matrix applied with v_bitop3 masks.
 #include <hip/hip_runtime.h>
@@ -239,12 +241,11 @@ struct Rs8RegArgs {
 // 8 elements per lane, so a workgroup holds 128 KiB of state and two
 // workgroups fit on a CU (one streams HBM while the other computes).
 //
-// Lane l: unit l&15, codeword (l>>4)&1, and index bit 0 of its elements = l>>5
-// ("sw").  Every other index bit is a register bit (3 per layout) or a wave bit,
-// so for any layer d >= 1 the butterfly partner is in the same lane and the
-// constant (a function of index bits > d) is wave-uniform: SGPR masks.  Layer
-// d = 0 pairs lanes l and l^32: both halves form T = x ^ y; the x half then adds
-// M*T (wave-uniform constant as well).
+// Lane l: index bit 0 of its elements = l&1 ("sw"), unit (l>>1)&15, codeword l>>5
+// (CDA_RS_DPP; the runtime-constant build keeps sw = l>>5).  Every other index bit
+// is a register bit (3 per layout) or a wave bit, so for any layer d >= 1 the
+// butterfly partner is in the same lane and the constant (a function of index
+// bits > d) is fixed per wave.  Layer d = 0 pairs lanes l and l^1 (d0_w).
 //   P1 f=1: IFFT d=0 (cross-lane), d=1..3 | exchange | P2 f=L-3: IFFT d=4..L-1,
 //   FFT d=L-1..L-3 | exchange | P3 f=1: FFT d=min(3,L-4)..1, d=0 (cross-lane).
 // ===========================================================================
