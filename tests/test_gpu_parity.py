@@ -668,3 +668,51 @@ def test_axis_root_order_error_wins_over_push_past(ctx):
     with pytest.raises(CdaError) as ei:
         ctx.nmt_axis_root(k, 0, good)
     assert ei.value.code == O.E_PUSH_PAST and ei.value.leaf == 2 * k
+
+
+_RS_DEVICE_SCRIPT = r"""
+import sys
+import numpy as np
+import torch  # first: libcda then resolves HIP through torch's runtime, as in bench.py
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import cda
+import oracle_lib as O
+ctx = cda.Context(0)
+dev = torch.device("cuda", 0)
+rng = np.random.default_rng(7)
+for k, ncw, L in [(16, 4, 512), (17, 4, 512), (34, 6, 512), (64, 2, 1024), (100, 4, 512), (128, 6, 512),
+                  (128, 3, 512), (126, 2, 512)]:
+    data = rng.integers(0, 256, (ncw, k, L), dtype=np.uint8)
+    d_src = torch.from_numpy(data).to(dev)
+    d_dst = torch.zeros((ncw, k, L), dtype=torch.uint8, device=dev)
+    # codeword c = data[c]: shards contiguous (the rows of erasureExtendSquare)
+    ctx.rs_encode_device(k, L, ncw, d_src.data_ptr(), k * L, L, d_dst.data_ptr(), k * L, L)
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy()
+    for c in range(ncw):
+        assert np.array_equal(got[c], O.leo_encode(data[c])), (k, ncw, L, c, "rows")
+    # the same codewords read as columns of a k x ncw grid (the column pass: src_cw = shard, src_sh = pitch)
+    grid = np.ascontiguousarray(data.transpose(1, 0, 2))  # [k][ncw][L]
+    d_src = torch.from_numpy(grid).to(dev)
+    d_dst = torch.zeros((k, ncw, L), dtype=torch.uint8, device=dev)
+    ctx.rs_encode_device(k, L, ncw, d_src.data_ptr(), L, ncw * L, d_dst.data_ptr(), L, ncw * L)
+    torch.cuda.synchronize()
+    got = d_dst.cpu().numpy().transpose(1, 0, 2)
+    for c in range(ncw):
+        assert np.array_equal(got[c], O.leo_encode(data[c])), (k, ncw, L, c, "cols")
+print("rs device ok")
+"""
+
+
+def test_rs_encode_device_batched_strided():
+    """cda_rs_encode_device, the batched strided Codec.Encode of the split path: even k (register encoder, incl.
+    non-powers of two whose padded elements are zero), odd k and odd codeword counts (LDS encoder), row- and
+    column-strided codewords, each codeword equal to the oracle's Leopard encode."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "celestia-app_amd")
+    out = subprocess.run([sys.executable, "-c", _RS_DEVICE_SCRIPT, pkg, here], capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0 and "rs device ok" in out.stdout, out.stderr[-3000:]
