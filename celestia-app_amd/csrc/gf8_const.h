@@ -1,14 +1,16 @@
 // gf8_const.h — the Leopard GF(2^8) FFT constants as compile-time values, and X ^= C*Y on bit-planes for a
 // compile-time C.
 //
-// The g2 encoder's P2 phase (rs_kernels.hip) keeps the top three index bits in registers, so every constant of its
-// layers is a function of template parameters only.  With the constant known to the compiler the multiply is the
-// 8x8 GF(2) matrix of C applied row by row (X[i] ^= XOR of the Y[j] with bit i of C*alpha^j set, two Y terms per
-// v_bitop3), about 18 VALU per butterfly instead of the ~45 of the branchy runtime-constant form (gf8_mul_asm.h).
+// The g2 encoder (rs_kernels.hip) keeps every index bit that a layer constant depends on in registers or in the
+// wave index, and instantiates one kernel body per wave index, so every constant of every layer is a compile-time
+// value.  A multiply by such a constant is its 8x8 GF(2) matrix in Leopard's own (Cantor) coordinates, emitted as a
+// straight program of 3-input XORs with shared terms factored out (gf8_prog): about 14 VALU per butterfly, against
+// ~45 VALU plus scalar branches for a runtime constant.
 //
 // The table is built by the same steps as leopard_tables.cpp (klauspost/reedsolomon v1.12.1 initConstants8 and
 // initFFT8), evaluated by the compiler; rs_init_device_tables checks it entry by entry against
-// the host-built table and refuses to initialise on any difference.
+// the host-built table and refuses to initialise on any difference, and tests/test_gf8_prog.py checks every program
+// against the oracle's Leopard multiply.
 #pragma once
 #include <stdint.h>
 
@@ -71,17 +73,6 @@ constexpr Cpoly8 make_cpoly8() {
 
 inline constexpr Cpoly8 kCpoly8 = make_cpoly8();
 
-// Row i of the multiply-by-C matrix in the standard basis: bit j set when bit i of C * alpha^j is set.
-constexpr unsigned gf8_row(unsigned c, int i) {
-  unsigned row = 0, v = c;
-  for (int j = 0; j < 8; j++) {
-    row |= ((v >> i) & 1u) << j;
-    v <<= 1;
-    if (v & 0x100) v ^= 0x11D;
-  }
-  return row;
-}
-
 constexpr int ctz8(unsigned v) {
   int n = 0;
   while (!(v & 1u)) {
@@ -95,40 +86,12 @@ __device__ __forceinline__ uint32_t xor3c(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// x ^= XOR of Y[j] over the set bits j of ROW, two terms per v_bitop3
-template <unsigned ROW>
-__device__ __forceinline__ void gf8_row_add(uint32_t& x, const uint32_t (&Y)[8]) {
-  if constexpr (ROW != 0) {
-    constexpr int j0 = ctz8(ROW);
-    constexpr unsigned rest = ROW & (ROW - 1);
-    if constexpr (rest == 0) {
-      x ^= Y[j0];
-    } else {
-      x = xor3c(x, Y[j0], Y[ctz8(rest)]);
-      gf8_row_add<rest & (rest - 1)>(x, Y);
-    }
-  }
-}
-
-// X ^= C * Y on 8 bit-planes (standard basis), C a compile-time constant
-template <unsigned C>
-__device__ __forceinline__ void gf8_muladd_const(uint32_t (&X)[8], const uint32_t (&Y)[8]) {
-  gf8_row_add<gf8_row(C, 0)>(X[0], Y);
-  gf8_row_add<gf8_row(C, 1)>(X[1], Y);
-  gf8_row_add<gf8_row(C, 2)>(X[2], Y);
-  gf8_row_add<gf8_row(C, 3)>(X[3], Y);
-  gf8_row_add<gf8_row(C, 4)>(X[4], Y);
-  gf8_row_add<gf8_row(C, 5)>(X[5], Y);
-  gf8_row_add<gf8_row(C, 6)>(X[6], Y);
-  gf8_row_add<gf8_row(C, 7)>(X[7], Y);
-}
-
 // ---- multiply in Leopard's own (Cantor) coordinates, with shared XOR terms ------------------------------------
-// Once every constant of the encoder is a compile-time value (rs_kernels.hip, P1/P2/P3), the basis only matters
-// through the density of the constants' matrices, and the Cantor basis (the byte bits themselves) is as dense as the
-// standard one for the FF8 constants (within 2 %), so the planes stay in Leopard's coordinates and the two basis
-// changes per element disappear.  Leopard's x*exp(L) is phi^-1(alpha^L * phi(x)); column j of its matrix is
-// phi^-1(c * phi(e_j)) with c = alpha^L in the standard basis (the kCpoly8 entry).
+// With every constant known at compile time the basis only matters through the density of the constants' matrices;
+// the Cantor basis (the byte bits themselves) is within 2 % of the standard one for the FF8 constants, so the planes
+// stay in Leopard's coordinates and no basis change is needed at load or store.  Leopard's x*exp(L) is
+// phi^-1(alpha^L * phi(x)); column j of its matrix is phi^-1(c * phi(e_j)) with c = alpha^L in the standard basis
+// (the kCpoly8 entry).
 constexpr unsigned gf8_mulstd(unsigned a, unsigned b) {
   unsigned r = 0;
   while (b) {

@@ -29,7 +29,6 @@
 
 #include "cda_internal.h"
 #include "gf8_const.h"
-#include "gf8_mul_asm.h"
 #include "gf_slice.h"
 #include "nmt_dev.h"
 
@@ -161,70 +160,12 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
   }
 }
 
-// ---- polynomial-basis arithmetic --------------------------------------------
-// Leopard's byte e is the Cantor-basis coordinate vector of phi(e) in the standard
-// field GF(2)[x]/(x^8+x^4+x^3+x^2+1), and exp(L) maps to alpha^L (alpha = x):
+// ---- Leopard's field --------------------------------------------------------
+// Leopard's byte e is the Cantor-basis coordinate vector of phi(e) in the standard field
+// GF(2)[x]/(x^8+x^4+x^3+x^2+1), and exp(L) maps to alpha^L (alpha = x):
 //   mul_leopard(a, b) = phi^-1(phi(a) * phi(b))      (checked in tests/test_oracle.py).
-// In the standard basis, multiplying 8 bit-planes by alpha is a plane rotation
-// plus 3 XORs, so x ^= c*y = XOR_{i: c_i} alpha^i*y costs 21 + 8*popcount(c)
-// full-rate v_xor with wave-uniform branches on c's bits -- no SGPR operands
-// (measured: VALU ops with an SGPR source issue at half rate on gfx950,
-// tools/valu_ubench.hip).
-__constant__ uint8_t c_cpoly8[256];  // per skew index: alpha^skew in std basis, 0 = no multiply
-
-// phi columns (phi(1<<j)):    {1, 214, 152, 146, 86, 200, 88, 230}
-// phi^-1 columns:              {1, 104, 92, 100, 114, 240, 86, 18}
-// (to_std8 / to_cantor8 below apply them to 8 bit-planes.)
-
-// The two basis changes of the g2 kernel as hand-scheduled XOR3 programs
-// (7 VALU each instead of 19 / 17 v_xor as a plain row-by-row XOR of the
-// matrices above); checked against the oracle by the GPU parity tests.
-__device__ __forceinline__ uint32_t xor3v(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ void to_std8(uint32_t (&v)[8]) {  // planes *= phi
-  const uint32_t t = xor3v(v[1], v[4], v[7]);
-  const uint32_t u = xor3v(v[1], v[2], v[3]);
-  const uint32_t o1 = t ^ v[3], o3 = xor3v(v[2], v[5], v[6]), o4 = xor3v(u, v[4], v[6]);
-  const uint32_t o6 = xor3v(t, v[5], v[6]), o7 = xor3v(u, v[5], v[7]), o5 = v[7];
-  v[1] = o1;
-  v[2] = t;
-  v[3] = o3;
-  v[4] = o4;
-  v[5] = o5;
-  v[6] = o6;
-  v[7] = o7;
-}
-__device__ __forceinline__ void to_cantor8(uint32_t (&v)[8]) {  // planes *= phi^-1
-  const uint32_t o1 = xor3v(v[4], v[6], v[7]), o2 = xor3v(v[2], v[3], v[6]), o3 = v[1] ^ v[2];
-  const uint32_t o4 = xor3v(o1, v[2], v[5]);
-  const uint32_t o5 = xor3v(v[1], v[3], v[4]) ^ v[5];
-  const uint32_t o6 = xor3v(o5, v[2], v[6]), o7 = v[5];
-  v[1] = o1;
-  v[2] = o2;
-  v[3] = o3;
-  v[4] = o4;
-  v[5] = o5;
-  v[6] = o6;
-  v[7] = o7;
-}
-
-// X ^= c * Y in the standard basis (c wave-uniform): gf8_muladd_asm, generated by
-// tools/gen_gf8_asm.py -- 21 v_xor for alpha^i * Y plus one v_xor / v_bitop3 XOR3 per
-// plane for each non-zero pair of bits of c.
-
-template <bool INVERSE>
-__device__ __forceinline__ void bfly_p(uint32_t (&X)[8], uint32_t (&Y)[8], unsigned c) {
-  if (INVERSE) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
-  }
-  if (c != 0u) gf8_muladd_asm(X, Y, c);
-  if (!INVERSE) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) Y[j] ^= X[j];
-  }
-}
+// The g2 encoder multiplies by compile-time constants only, so it works directly on
+// Leopard's coordinates with each constant's matrix (gf8_const.h).
 
 struct Rs8RegArgs {
   const uint8_t* src;
@@ -241,8 +182,8 @@ struct Rs8RegArgs {
 // 8 elements per lane, so a workgroup holds 128 KiB of state and two
 // workgroups fit on a CU (one streams HBM while the other computes).
 //
-// Lane l: index bit 0 of its elements = l&1 ("sw"), unit (l>>1)&15, codeword l>>5
-// (CDA_RS_DPP; the runtime-constant build keeps sw = l>>5).  Every other index bit
+// Lane l: index bit 0 of its elements = l&1 ("sw"), unit (l>>1)&15, codeword l>>5.
+// Every other index bit
 // is a register bit (3 per layout) or a wave bit, so for any layer d >= 1 the
 // butterfly partner is in the same lane and the constant (a function of index
 // bits > d) is fixed per wave.  Layer d = 0 pairs lanes l and l^1 (d0_w).
@@ -253,36 +194,6 @@ __host__ __device__ constexpr int x2_of(int w, int sw, int r, int f) {
   // bits 1..L-1 of the element index: 3 register bits at (f..f+2), wave bits elsewhere
   const int y = ((w >> (f - 1)) << (f + 2)) | (r << (f - 1)) | (w & ((1 << (f - 1)) - 1));
   return (y << 1) | sw;
-}
-
-template <bool INVERSE, int M>
-__device__ __forceinline__ void layer2_u(uint32_t (&E)[8][8], int w, int f, int d) {
-  const int rb = d - f;
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    if (r & (1 << rb)) continue;
-    const int x = x2_of(w, 0, r, f);
-    const int s0 = (x >> (d + 1)) << (d + 1);
-    const int idx = INVERSE ? (M - 1 + s0 + (1 << d)) : (s0 + (1 << d) - 1);
-    bfly_p<INVERSE>(E[r], E[r | (1 << rb)], c_cpoly8[idx]);
-  }
-}
-
-#ifndef CDA_RS_WCONST
-#define CDA_RS_WCONST 1
-#endif
-// CDA_RS_CANTOR: planes in Leopard's own coordinates (no basis change at load / store), every multiply a
-// compile-time matrix program (gf8_const.h gf8_muladd_cantor); needs the specialised P1 / P3 (CDA_RS_WCONST).
-#ifndef CDA_RS_CANTOR
-#define CDA_RS_CANTOR CDA_RS_WCONST
-#endif
-static_assert(!CDA_RS_CANTOR || CDA_RS_WCONST, "the Cantor-coordinate encoder has no runtime-constant multiply");
-template <unsigned C>
-__device__ __forceinline__ void gf8_muladd_k(uint32_t (&X)[8], const uint32_t (&Y)[8]) {
-  if constexpr (CDA_RS_CANTOR)
-    gf8_muladd_cantor<C>(X, Y);
-  else
-    gf8_muladd_const<C>(X, Y);
 }
 
 // P2 layers (register bits F..F+2 = the top three index bits, d >= F): every index bit above d is a register
@@ -302,7 +213,7 @@ __device__ __forceinline__ void bfly_const(uint32_t (&E)[8][8]) {
 #pragma unroll
       for (int j = 0; j < 8; j++) Y[j] ^= X[j];
     }
-    if constexpr (c != 0u) gf8_muladd_k<c>(X, Y);
+    if constexpr (c != 0u) gf8_muladd_cantor<c>(X, Y);
     if (!INVERSE) {
 #pragma unroll
       for (int j = 0; j < 8; j++) Y[j] ^= X[j];
@@ -339,43 +250,18 @@ __device__ __forceinline__ void p2_layers(uint32_t (&E)[8][8]) {
   }
 }
 
-// d = 0 across lane halves (element x in lanes 0..31, x+1 in lanes 32..63).
-// v_permlane32_swap(a, a) hands every lane both x (lanes 0..31's a) and y (lanes
-// 32..63's a); both halves compute the butterfly, and a second swap puts x' back
-// in the low half and y' in the high half.  No LDS, no lane selects.
-template <bool INVERSE, int M>
-__device__ __forceinline__ void layer2_d0(uint32_t (&E)[8][8], int w, int f, bool upper) {
-  (void)upper;
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    const int x = x2_of(w, 0, r, f);
-    const unsigned c = c_cpoly8[INVERSE ? (M - 1 + x + 1) : x];
-    uint32_t X[8], Y[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const auto p = __builtin_amdgcn_permlane32_swap(E[r][j], E[r][j], false, false);
-      X[j] = p[0];
-      Y[j] = p[1];
-    }
-    bfly_p<INVERSE>(X, Y, c);
-#pragma unroll
-    for (int j = 0; j < 8; j++) E[r][j] = __builtin_amdgcn_permlane32_swap(X[j], Y[j], false, false)[0];
-  }
-}
-
 // ---- P1 / P3 with compile-time constants ------------------------------------
 // In the f = 1 layout the constants of layers d = 0..3 are functions of the register bits and of the wave
 // index w (bits 4..L-1).  w is wave-uniform, so a scalar branch on it selects a copy of P1 / P3 specialised for
-// that wave, where every constant is again a compile-time value (the GF(2)-matrix multiply of gf8_const.h,
-// ~18 VALU) instead of the runtime form (gf8_mul_asm.h, ~45 VALU + scalar branches).  Costs code size:
-// 2^(L-4) copies of P1 and P3.
+// that wave, where every constant is again a compile-time value (the XOR3 program of gf8_const.h, ~14 VALU,
+// instead of ~45 VALU + scalar branches for a runtime constant).  Costs code size: 2^(L-4) kernel bodies.
 template <bool INVERSE, unsigned C>
 __device__ __forceinline__ void bfly_cc(uint32_t (&X)[8], uint32_t (&Y)[8]) {
   if (INVERSE) {
 #pragma unroll
     for (int j = 0; j < 8; j++) Y[j] ^= X[j];
   }
-  if constexpr (C != 0u) gf8_muladd_k<C>(X, Y);
+  if constexpr (C != 0u) gf8_muladd_cantor<C>(X, Y);
   if (!INVERSE) {
 #pragma unroll
     for (int j = 0; j < 8; j++) Y[j] ^= X[j];
@@ -407,15 +293,12 @@ __device__ __forceinline__ void layer_w(uint32_t (&E)[8][8]) {
   bfly_w<INVERSE, M, W, D, 7>(E);
 }
 
-// layer d = 0, wave W.  With the specialised phases the element index bit 0 sits on lane bit 0 (CDA_RS_DPP), so a
-// butterfly's two elements are in lanes 2i and 2i+1 and one DPP quad_perm read hands each lane its partner's plane,
+// layer d = 0, wave W.  The element index bit 0 sits on lane bit 0, so a butterfly's two elements are in lanes 2i and 2i+1 and one DPP quad_perm read hands each lane its partner's plane,
 // folded into the XOR.  Each lane computes only its own output; `lm` is all-ones in the x (even) lanes:
 //   IFFT: T = x ^ y;  x' = x ^ c*T, y' = T                      (c*T computed wave-wide, kept in x lanes)
 //   FFT:  S = y (own or partner), T = x ^ y;  x' = x ^ c*S, y' = T ^ c*S = (lm ? x : T) ^ c*S
-// Without CDA_RS_DPP (lane bit 5): v_permlane32_swap hands both halves both elements, both compute the butterfly.
-#ifndef CDA_RS_DPP
-#define CDA_RS_DPP CDA_RS_WCONST
-#endif
+// (Round 1 kept bit 0 on lane bit 5: two v_permlane32_swap + copies per plane, both halves computing the whole
+// butterfly -- about twice the VALU of this form.)
 __device__ __forceinline__ uint32_t lane_pair_xor(uint32_t v) {  // v ^ v[lane ^ 1]
   return v ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
 }
@@ -440,7 +323,7 @@ template <bool INVERSE, int M, int W, int R>
 __device__ __forceinline__ void d0_w(uint32_t (&E)[8][8], uint32_t lm) {
   constexpr int x = x2_of(W, 0, R, 1);
   constexpr unsigned c = kCpoly8.v[INVERSE ? (M - 1 + x + 1) : x];
-  if constexpr (CDA_RS_DPP) {
+  {
     uint32_t T[8];
     if constexpr (INVERSE) {
 #pragma unroll
@@ -449,7 +332,7 @@ __device__ __forceinline__ void d0_w(uint32_t (&E)[8][8], uint32_t lm) {
       lane_pair_xor8(T, E[R]);
     }
     if constexpr (INVERSE) {
-      if constexpr (c != 0u) gf8_muladd_k<c>(E[R], T);
+      if constexpr (c != 0u) gf8_muladd_cantor<c>(E[R], T);
 #pragma unroll
       for (int j = 0; j < 8; j++) E[R][j] = __builtin_amdgcn_bitop3_b32(lm, E[R][j], T[j], 0xCA);  // lm ? E : T
     } else {
@@ -459,23 +342,12 @@ __device__ __forceinline__ void d0_w(uint32_t (&E)[8][8], uint32_t lm) {
         S[j] = __builtin_amdgcn_bitop3_b32(E[R][j], T[j], lm, 0x78);       // E ^ (T & lm) = y
         E[R][j] = __builtin_amdgcn_bitop3_b32(lm, E[R][j], T[j], 0xCA);    // lm ? x : T
       }
-      if constexpr (c != 0u) gf8_muladd_k<c>(E[R], S);
+      if constexpr (c != 0u) gf8_muladd_cantor<c>(E[R], S);
     }
     // pin the results here: otherwise the compiler sinks this arithmetic into the (conditional) store blocks
     // while the DPP reads stay put, and every butterfly's T / S stays live until the stores
 #pragma unroll
     for (int j = 0; j < 8; j++) asm volatile("" : "+v"(E[R][j]));
-  } else {
-    uint32_t X[8], Y[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const auto p = __builtin_amdgcn_permlane32_swap(E[R][j], E[R][j], false, false);
-      X[j] = p[0];
-      Y[j] = p[1];
-    }
-    bfly_cc<INVERSE, c>(X, Y);
-#pragma unroll
-    for (int j = 0; j < 8; j++) E[R][j] = __builtin_amdgcn_permlane32_swap(X[j], Y[j], false, false)[0];
   }
   __builtin_amdgcn_sched_barrier(0);  // one butterfly's temporaries live at a time
 }
@@ -536,18 +408,14 @@ __device__ __forceinline__ void exchange2(uint32_t (&E)[8][8], uint4* xbuf, int 
   }
 }
 
-// Work of workgroup `wg` (blockDim = 64 << (L - 4)); xbuf = [M][32] x 16 B LDS (L > 4).
-// WC >= 0: the body of wave w == WC with P1 / P3 specialised for it; WC < 0: runtime constants.
+// Work of workgroup `wg` (blockDim = 64 << (L - 4)) for its wave WC (== w); xbuf = [M][32] x 16 B LDS (L > 4).
 template <int L, int WC>
 __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* xbuf, int w) {
   constexpr int M = 1 << L;
   const int lane = threadIdx.x & 63;
-  // lane = (li, sw): sw = element index bit 0 on lane bit 0 (DPP pairs) or lane bit 5 (permlane32 halves);
-  // li = unit u (16) and codeword cwi (2)
-  constexpr int SWB = (CDA_RS_DPP && WC >= 0) ? 0 : 5;
-  const int sw = (lane >> SWB) & 1, li = SWB == 0 ? lane >> 1 : lane & 31;
+  // lane = (li, sw): sw = element index bit 0 (DPP pairs), li = unit u (16) and codeword cwi (2)
+  const int sw = lane & 1, li = lane >> 1;
   const int u = li & 15, cwi = li >> 4;
-  const bool upper = sw != 0;
   uint32_t lm = sw ? 0u : ~0u;  // x lanes of the d = 0 butterflies
   asm volatile("" : "+v"(lm));
   const int slice = wg % a.slices;
@@ -565,7 +433,7 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
 
   uint32_t E[8][8];
   const SliceMasks km = slice_masks();
-  const int wv = WC >= 0 ? WC : w;
+  constexpr int wv = WC;
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     // x0 (the pair's even element) is wave-uniform and, k being even on this path, x < k iff x0 < k: the branch is
@@ -582,7 +450,6 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
       E[r][0] = v0.x; E[r][1] = v0.y; E[r][2] = v0.z; E[r][3] = v0.w;
       E[r][4] = v1.x; E[r][5] = v1.y; E[r][6] = v1.z; E[r][7] = v1.w;
       bitslice8(E[r], km);
-      if constexpr (!CDA_RS_CANTOR) to_std8(E[r]);  // Cantor coordinates -> standard basis
     } else {
 #pragma unroll
       for (int j = 0; j < 8; j++) E[r][j] = 0;
@@ -590,25 +457,13 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
   }
   constexpr int F2 = L - 3;  // P2 register bits F2..F2+2 = L-3..L-1
   // P1 (f=1): IFFT d=0 (cross-lane), d=1..3 (or up to L-1 when L == 4)
-  if constexpr (WC >= 0) {
-    p1_w<L, WC>(E, lm);
-  } else {
-    layer2_d0<true, M>(E, w, 1, upper);
-#pragma unroll
-    for (int d = 1; d < 4 && d < L; d++) layer2_u<true, M>(E, w, 1, d);
-  }
-  if (L > 4) exchange2<M>(E, xbuf, w, sw, li, 1, F2);
+  p1_w<L, WC>(E, lm);
+  if (L > 4) exchange2<M>(E, xbuf, WC, sw, li, 1, F2);
   // P2: IFFT d=4..L-1, FFT d=L-1..F2 (compile-time constants)
   p2_layers<L, (F2 > 1 ? F2 : 1), 4, true>(E);
-  if (L > 4) exchange2<M>(E, xbuf, w, sw, li, F2, 1);
+  if (L > 4) exchange2<M>(E, xbuf, WC, sw, li, F2, 1);
   // P3 (f=1): FFT d=F2-1..1, then d=0 (cross-lane)
-  if constexpr (WC >= 0) {
-    p3_w<L, WC>(E, lm);
-  } else {
-#pragma unroll
-    for (int d = (F2 - 1 < 3 ? F2 - 1 : 3); d >= 1; d--) layer2_u<false, M>(E, w, 1, d);
-    layer2_d0<false, M>(E, w, 1, upper);
-  }
+  p3_w<L, WC>(E, lm);
   const SliceMasks ko = slice_masks();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
@@ -617,7 +472,6 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
       uint32_t v[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) v[j] = E[r][j];
-      if constexpr (!CDA_RS_CANTOR) to_cantor8(v);  // standard basis -> Cantor coordinates
       bitslice8(v, ko);
       uint4* q = reinterpret_cast<uint4*>(dst + x * a.dst_sh);
       q[0] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -642,10 +496,7 @@ __device__ __forceinline__ void rs_g2_select(const Rs8RegArgs& a, int wg, uint4*
 template <int L>
 __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* xbuf) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & ((1 << (L - 4)) - 1);
-  if constexpr (CDA_RS_WCONST)
-    rs_g2_select<L, 0>(a, wg, xbuf, w);
-  else
-    rs_g2_impl<L, -1>(a, wg, xbuf, w);
+  rs_g2_select<L, 0>(a, wg, xbuf, w);
 }
 
 template <int L>
@@ -815,7 +666,6 @@ int rs_init_device_tables(int device) {
   for (int i = 0; i < 256; i++) cpoly[i] = skew[i] >= 255 ? 0 : apow[skew[i]];
   for (int i = 0; i < 256; i++)
     if (cpoly[i] != kCpoly8.v[i]) return -1;  // the encoder's compile-time constants (gf8_const.h)
-  if (hipMemcpyToSymbol(HIP_SYMBOL(c_cpoly8), cpoly, sizeof cpoly) != hipSuccess) return -1;
   if (hipFuncSetAttribute((const void*)rs_encode8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
       hipSuccess)
     return -1;
