@@ -37,6 +37,12 @@ namespace cda {
 __constant__ uint16_t c_skew8[256];
 __constant__ unsigned long long c_col8[256];
 
+// LDS bank swizzle of the plane-major state of the LDS encoders ([plane][m*U] words, element e = x*U + u).  In a
+// layer D the 32 lanes of a half-wave touch e with one bit fixed (bit log2(D*U)) and bits 0..5 otherwise free, so for
+// D*U < 32 two lanes whose e differ in bit 5 only land in the same bank (2-way conflicts in every low layer).
+// Flipping bits 0..4 when bit 5 is set separates them for any fixed bit, and keeps contiguous runs conflict-free.
+__device__ __forceinline__ int lds_sw(int e) { return e ^ (((e >> 5) & 1) * 31); }
+
 // x ^= M * y, M(j,b) = bit (8b+j) of cb
 __device__ __forceinline__ void gf8_muladd(uint32_t x[8], const uint32_t y[8], unsigned long long cb) {
 #pragma unroll
@@ -57,8 +63,8 @@ __device__ __forceinline__ void butterfly8(uint32_t* st, int mU, int U, int x, i
   uint32_t X[8], Y[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    X[j] = st[j * mU + x * U + u];
-    Y[j] = st[j * mU + y * U + u];
+    X[j] = st[j * mU + lds_sw(x * U + u)];
+    Y[j] = st[j * mU + lds_sw(y * U + u)];
   }
   if (INVERSE) {  // IFFT2
 #pragma unroll
@@ -71,8 +77,8 @@ __device__ __forceinline__ void butterfly8(uint32_t* st, int mU, int U, int x, i
   }
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    st[j * mU + x * U + u] = X[j];
-    st[j * mU + y * U + u] = Y[j];
+    st[j * mU + lds_sw(x * U + u)] = X[j];
+    st[j * mU + lds_sw(y * U + u)] = Y[j];
   }
 }
 
@@ -140,7 +146,7 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
       for (int j = 0; j < 8; j++) w[j] = 0;
     }
 #pragma unroll
-    for (int j = 0; j < 8; j++) st[j * (a.m << a.log2U) + s * U + u] = w[j];
+    for (int j = 0; j < 8; j++) st[j * (a.m << a.log2U) + lds_sw(s * U + u)] = w[j];
   }
   __syncthreads();
   // IFFT (data at points m..m+k-1), D = 1 .. m/2
@@ -152,7 +158,7 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
     const int s = e >> a.log2U, u = e & (U - 1);
     uint32_t w[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) w[j] = st[j * (a.m << a.log2U) + s * U + u];
+    for (int j = 0; j < 8; j++) w[j] = st[j * (a.m << a.log2U) + lds_sw(s * U + u)];
     bitslice8(w);
     uint4* q = reinterpret_cast<uint4*>(dst + s * a.dst_sh + u * 32);
     q[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -830,8 +836,8 @@ __device__ __forceinline__ void butterfly16(uint32_t* st, int mU, int U, int x, 
   uint32_t X[16], Y[16];
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    X[j] = st[j * mU + x * U + u];
-    Y[j] = st[j * mU + y * U + u];
+    X[j] = st[j * mU + lds_sw(x * U + u)];
+    Y[j] = st[j * mU + lds_sw(y * U + u)];
   }
   if (INVERSE) {
 #pragma unroll
@@ -848,8 +854,8 @@ __device__ __forceinline__ void butterfly16(uint32_t* st, int mU, int U, int x, 
   }
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    st[j * mU + x * U + u] = X[j];
-    st[j * mU + y * U + u] = Y[j];
+    st[j * mU + lds_sw(x * U + u)] = X[j];
+    st[j * mU + lds_sw(y * U + u)] = Y[j];
   }
 }
 
@@ -922,7 +928,7 @@ __global__ void __launch_bounds__(256) rs_encode16_kernel(Rs16Args a) {
       for (int j = 0; j < 16; j++) v[j] = 0;
     }
 #pragma unroll
-    for (int j = 0; j < 16; j++) st[j * mU + s * U + u] = v[j];
+    for (int j = 0; j < 16; j++) st[j * mU + lds_sw(s * U + u)] = v[j];
   }
   __syncthreads();
   for (int lD = 0; lD < a.log2m; lD++) rs_layer16<true>(st, a, 1 << lD, lD);
@@ -931,7 +937,7 @@ __global__ void __launch_bounds__(256) rs_encode16_kernel(Rs16Args a) {
     const int s = e >> a.log2U, u = e & (U - 1);
     uint32_t v[16];
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = st[j * mU + s * U + u];
+    for (int j = 0; j < 16; j++) v[j] = st[j * mU + lds_sw(s * U + u)];
     apply16(v, kPhiInv16);
     uint32_t lo[8], hi[8];
 #pragma unroll
