@@ -251,8 +251,13 @@ def pmc_counters(kernel, B):
         if not c:
             continue
         scale = B / float(c.get("bench_batch", PMC_BATCH))
+        busy = None
+        if c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
+            # SQ_ACTIVE_INST_VALU: quad-cycles of VALU issue summed over the 1024 SIMDs; GRBM_GUI_ACTIVE: cycles x 8 XCDs
+            busy = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * c["GRBM_GUI_ACTIVE"] / 8)
         return {"hbm_bytes": int(c["hbm_bytes_corrected"] * scale) if "hbm_bytes_corrected" in c else None,
                 "valu_insts": c["SQ_INSTS_VALU"] * scale if "SQ_INSTS_VALU" in c else None,
+                "valu_busy": busy,
                 "source": f"{os.path.relpath(f, ROOT)} ({PMC_NAMES[kernel]}, B={c.get('bench_batch', PMC_BATCH)} "
                           f"profile scaled to B={B})"}
     return None
@@ -647,6 +652,10 @@ def main():
                                      "(int32 lane-ops/s)",
                          "hbm": {"achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK, "unit": "GB/s",
                                  "frac": round(hbm_gbs / HBM_PEAK, 4) if hbm_gbs else None},
+                         "valu_busy_pmc": round(pmc["valu_busy"], 3) if pmc.get("valu_busy") else None,
+                         "valu_busy_def": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x kernel cycles): fraction of the "
+                                          "kernel's cycles the VALU was issuing; frac < busy because 57 % of SHA-256's "
+                                          "instructions take 4 cycles, not 2 (DESIGN.md §4)",
                          "counters_source": pmc["source"]})
     else:  # no PMC pass covers this kernel: HBM view only
         roofline.update({"bound": "hbm", "achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK,
