@@ -34,6 +34,8 @@ E_PUSH_PAST = -11
 E_UNSUPPORTED = -12
 E_SHARE_VERSION = -13
 E_BLOB_SIZE = -14
+E_NOMEM = -15
+E_INTERNAL = -16
 
 AXIS_ROW = 0
 AXIS_COL = 1
@@ -48,7 +50,8 @@ EXPORTS = [
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
     "cda_blob_commitments", "cda_merkle_roots", "cda_extend_commit_nodes", "cda_share_inclusion_proof",
     "cda_host_alloc", "cda_host_free", "cda_multi_init", "cda_multi_free", "cda_multi_device_count",
-    "cda_multi_context", "cda_multi_extend_commit_batch", "cda_build_ods_device", "cda_construct_extend_commit",
+    "cda_multi_context", "cda_multi_device", "cda_multi_extend_commit_batch", "cda_build_ods_device",
+    "cda_construct_extend_commit",
 ]
 
 
@@ -127,6 +130,7 @@ def lib():
                 "cda_multi_free": (None, [P]),
                 "cda_multi_device_count": (I32, [P]),
                 "cda_multi_context": (P, [P, I32]),
+                "cda_multi_device": (I32, [P, I32]),
                 "cda_multi_extend_commit_batch": (I32, [P, U32, U32, P, P, P, P, P, P]),
                 "cda_build_ods_device": (I32, [P, U32, U32, P, P, U64, P, U32, P, P]),
                 "cda_construct_extend_commit": (I32, [P, U32, U32, P, P, U64, P, U32, P, P, P, P, P, P]),
@@ -150,8 +154,8 @@ def _p(a):
 def _check(rc, err=None, ctx=None):
     if rc == OK:
         return
-    if rc == E_DEVICE and ctx is not None:
-        raise CdaError(rc, "device error: " + lib().cda_last_device_error(ctx._h).decode())
+    if rc in (E_DEVICE, E_NOMEM, E_INTERNAL) and ctx is not None:
+        raise CdaError(rc, strerror(rc) + ": " + lib().cda_last_device_error(ctx._h).decode())
     if err is not None:
         raise CdaError(rc, axis=err.axis, index=err.index, leaf=err.leaf, block=err.block)
     raise CdaError(rc)

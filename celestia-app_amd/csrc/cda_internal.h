@@ -52,13 +52,6 @@ int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d
                      int ncw, int k, int shard_len, hipStream_t s);
 int launch_rs_encode8(const RsJob& job, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
-// Extension fused with leaf hashing (block path, k = 16..128, 512-B shares): the rows kernel writes
-// Q0 copy + Q1 and the leaf records of the top half (push order checked against the ODS into
-// d_status), the cols kernel writes Q2|Q3 and the leaf records of the bottom half.
-bool rs_leaf_fusable(int k);
-int launch_rs_rows_leaf(const RsJob& rows, const uint8_t* d_ods, const uint8_t* d_eds, void* d_nodes,
-                        unsigned long long* d_status, hipStream_t s);
-int launch_rs_cols_leaf(const RsJob& cols, const uint8_t* d_eds, void* d_nodes, hipStream_t s);
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
                      hipStream_t s);
 int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int nblocks, int level, hipStream_t s);

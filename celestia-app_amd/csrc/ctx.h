@@ -6,6 +6,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cda_internal.h"
@@ -18,26 +19,12 @@ struct cda_ctx {
   int device = 0;
   std::recursive_mutex mu;
   hipStream_t stream = nullptr;
-  // sub-batch streams: independent blocks of one call are split across these so
-  // that one sub-batch's memory-bound RS phase and latency-bound tree tail overlap
-  // another's hashing (no dependency between blocks).
-  static constexpr int kMaxSub = 8;
-  int nsub = 1;
-  // CDA_PIPELINE: chunks of a batch software-pipelined over two streams (RS of chunk i+1
-  // overlaps the hashing of chunk i); 1 = off.
-  int pipe_chunks = 1;
-  // CDA_CHUNK: blocks per sequential chunk on one stream (0 = whole batch at once)
-  int chunk_blocks = 0;
-  // CDA_FUSED=1: extension fused with leaf hashing (measured no faster; see rs_kernels.hip)
-  bool fused = false;
   // CDA_REPAIR_OVERLAP=0: repair verifies each batch on the decode stream instead of a second stream
   bool repair_overlap = true;
   // CDA_REPAIR_FUSED=0: verify with the generic leaf + per-level launches instead of one fused launch
   bool repair_fused_verify = true;
   // CDA_REPAIR_EARLY=0: repair copies the square back only at the end (no early row return)
   bool repair_early = true;
-  hipStream_t sub[kMaxSub] = {};  // created on first use (ensure_sub): experiment paths only
-  bool sub_ready = false;
   // HIP maps streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues, so the streams that must run
   // concurrently are created first, together: stream, h2d_stream, d2h_stream, aux_stream.
   hipStream_t aux_stream = nullptr;
@@ -51,7 +38,9 @@ struct cda_ctx {
   static constexpr int kSlots = 3;
   hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;
   hipEvent_t ev_h2d[kSlots] = {}, ev_comp[kSlots] = {}, ev_d2h[kSlots] = {};
-  hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
+  // fork / join of repair's verification streams
+  static constexpr int kJoin = 2;
+  hipEvent_t fork_ev = nullptr, join_ev[kJoin] = {};
   std::string last_err;
   // workspace
   struct Buf {
@@ -100,7 +89,6 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
 int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
                     uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err, int block0);
 int ensure_pipeline(cda_ctx* c);  // copy streams + per-slot events (host_pipeline.cpp)
-int ensure_sub(cda_ctx* c);       // the CDA_STREAMS / CDA_PIPELINE sub-streams (engine.cpp)
 void free_pipeline(cda_ctx* c);
 // Caller-memory copies (staging.cpp): large pageable buffers through the pinned rings, pinned / small ones
 // directly.  staged_h2d returns once the source may be released (DMA enqueued on s); staged_d2h once the
@@ -110,6 +98,38 @@ int staged_d2h(cda_ctx* c, void* h_dst, const void* d_src, size_t n, hipStream_t
 void free_staging(cda_ctx* c);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
+
+// ---- exception barrier of the C ABI ----
+// No C++ exception may cross an extern "C" entry point: under cgo it reaches std::terminate inside the Go node,
+// where neither ProcessProposal's recover() (app/process_proposal.go:28-34) nor any caller can handle it.  Every
+// entry point wraps its body in CDA_API_TRY / CDA_API_CATCH(ctx): std::bad_alloc -> CDA_E_NOMEM, anything else
+// (std::system_error from a thread start, ...) -> CDA_E_INTERNAL, with what() in cda_last_device_error.
+int api_exception(cda_ctx* c) noexcept;  // call from a catch block: classifies the exception in flight
+// Failure injection for tests: CDA_FAULT_INJECT=<site> throws at that site -- "entry" (every entry point, before
+// its body), "alloc" (device workspace growth, as std::bad_alloc), "thread" (a helper-thread start, as
+// std::system_error).  Unset in production; one getenv per call.
+void fault_point(const char* site);
+#define CDA_API_TRY try { ::cda::fault_point("entry");
+#define CDA_API_CATCH(ctx) \
+  }                        \
+  catch (...) { return ::cda::api_exception(ctx); }
+
+// Joins helper threads on every exit path (an exception between two thread starts would otherwise destroy a
+// joinable std::thread, i.e. std::terminate); `stop` runs first so that blocked helpers can leave.
+template <class Stop>
+struct ThreadJoiner {
+  std::vector<std::thread*> ts;
+  Stop stop;
+  explicit ThreadJoiner(Stop s) : stop(s) {}
+  ~ThreadJoiner() {
+    bool any = false;
+    for (auto* t : ts) any = any || t->joinable();
+    if (!any) return;
+    stop();
+    for (auto* t : ts)
+      if (t->joinable()) t->join();
+  }
+};
 
 // Synchronous entry points (work on c->stream): ordered after any device-resident enqueue.
 struct Lock {

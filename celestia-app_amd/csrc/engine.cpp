@@ -23,6 +23,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -68,8 +69,38 @@ bool dev_ok(cda_ctx* c, hipError_t e, const char* what) {
   return false;
 }
 
+int api_exception(cda_ctx* c) noexcept {
+  int code = CDA_E_INTERNAL;
+  const char* what = "unknown exception";
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    code = CDA_E_NOMEM;
+    what = "out of host memory (std::bad_alloc)";
+  } catch (const std::exception& ex) {
+    what = ex.what();
+  } catch (...) {
+  }
+  if (c) {
+    try {
+      c->last_err = what;
+    } catch (...) {
+    }
+  }
+  return code;
+}
+
+void fault_point(const char* site) {
+  const char* e = getenv("CDA_FAULT_INJECT");
+  if (!e || strcmp(e, site) != 0) return;
+  if (strcmp(site, "thread") == 0)
+    throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again), "injected thread failure");
+  throw std::bad_alloc();
+}
+
 int ensure(cda_ctx* c, cda_ctx::Buf& b, size_t bytes) {
   if (b.cap >= bytes) return CDA_OK;
+  fault_point("alloc");
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.cap = 0;
@@ -200,110 +231,19 @@ int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ed
   return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, rec_off);
 }
 
-int enqueue_pipeline_one(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
-                         void* d_dah, unsigned long long* d_status, hipStream_t s, size_t rec_off) {
-  if (c->fused && rs_leaf_fusable((int)k)) {
-    // extension fused with leaf hashing: rows (Q0 copy + Q1 + top-half leaves), cols (Q2|Q3 + bottom leaves)
-    if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
-    {
-      ProfScope ps(c, "rs_rows_leaf", s);
-      if (launch_rs_rows_leaf(rows_job(k, nblocks, d_ods, d_eds), d_ods, d_eds, bufs0(c, rec_off), d_status, s))
-        return CDA_E_DEVICE;
-    }
-    {
-      ProfScope ps(c, "rs_cols_leaf", s);
-      if (launch_rs_cols_leaf(cols_job(k, nblocks, d_eds), d_eds, bufs0(c, rec_off), s)) return CDA_E_DEVICE;
-    }
-    return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, rec_off);
-  }
-  if (int rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s)) return rc;
-  return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, rec_off);
-}
-
-// Pipeline over nblocks on `s`; with nsub > 1 (CDA_STREAMS) independent chunks of
-// blocks go to sub-streams forked from / joined back into `s` (serial while
-// profiling so per-kernel event timings do not overlap).  Measured on MI355X:
-// one stream is as fast or faster (each kernel already fills the GPU), and
-// CU-masked streams (RS on some CUs, SHA on the rest) were 2-5x slower.
-int ensure_sub(cda_ctx* c) {
-  if (c->sub_ready) return CDA_OK;
-  for (int i = 0; i < cda_ctx::kMaxSub; i++)
-    if (!c->sub[i] && !dev_ok(c, hipStreamCreateWithFlags(&c->sub[i], hipStreamNonBlocking), "hipStreamCreate"))
-      return CDA_E_DEVICE;
-  c->sub_ready = true;
-  return CDA_OK;
-}
-
 int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                      void* d_dah, unsigned long long* d_status, hipStream_t s) {
+  // One stream, one kernel per stage: each stage already fills the GPU.  Measured slower and removed
+  // (DESIGN.md §4 "Scheduling experiments"): sub-streams over independent chunks, a two-stream RS/SHA
+  // software pipeline, sequential Infinity-Cache-sized chunks, CU-masked streams, RS fused with leaf hashing.
   const uint32_t w = 2 * k;
   const size_t cells = (size_t)nblocks * w * w;
   int rc = ensure(c, c->leaf, cells * CDA_REC_BYTES);
   if (rc) return rc;
   rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES);  // inner tree levels
   if (rc) return rc;
-  if (!c->prof && c->pipe_chunks > 1 && nblocks > 1) {
-    // Two-stream software pipeline: stream sub[0] runs the RS phase chunk after chunk,
-    // stream sub[1] hashes chunk i as soon as its RS phase is done, so the memory-bound
-    // RS of chunk i+1 overlaps the VALU-bound hashing of chunk i.
-    const uint32_t C = std::min<uint32_t>((uint32_t)c->pipe_chunks, nblocks);
-    if ((rc = ensure_sub(c))) return rc;
-    hipStream_t srs = c->sub[0], ssha = c->sub[1];
-    if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord") ||
-        !dev_ok(c, hipStreamWaitEvent(srs, c->fork_ev, 0), "hipStreamWaitEvent") ||
-        !dev_ok(c, hipStreamWaitEvent(ssha, c->fork_ev, 0), "hipStreamWaitEvent"))
-      return CDA_E_DEVICE;
-    uint32_t done = 0;
-    for (uint32_t i = 0; i < C; i++) {
-      const uint32_t nb = (nblocks - done) / (C - i);
-      const uint8_t* o = d_ods + (size_t)done * k * k * CDA_SHARE;
-      uint8_t* e = d_eds + (size_t)done * w * w * CDA_SHARE;
-      if (int rc2 = enqueue_rs(c, k, nb, o, e, srs)) return rc2;
-      if (!dev_ok(c, hipEventRecord(c->join_ev[0], srs), "hipEventRecord") ||
-          !dev_ok(c, hipStreamWaitEvent(ssha, c->join_ev[0], 0), "hipStreamWaitEvent"))
-        return CDA_E_DEVICE;
-      if (int rc2 = enqueue_commit(c, k, nb, e, (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES,
-                                   (uint8_t*)d_dah + (size_t)done * 32, d_status + done, ssha, (size_t)done * w * w))
-        return rc2;
-      done += nb;
-    }
-    if (!dev_ok(c, hipEventRecord(c->join_ev[1], ssha), "hipEventRecord") ||
-        !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[1], 0), "hipStreamWaitEvent"))
-      return CDA_E_DEVICE;
-    return CDA_OK;
-  }
-  if (c->chunk_blocks > 0 && (uint32_t)c->chunk_blocks < nblocks) {
-    // Sequential chunks on one stream: every phase of a chunk runs before the next chunk, so a chunk's
-    // working set (EDS + records) can stay in the 256 MB Infinity Cache between its phases.
-    for (uint32_t done = 0; done < nblocks;) {
-      const uint32_t nb = std::min<uint32_t>((uint32_t)c->chunk_blocks, nblocks - done);
-      if (int rc2 = enqueue_pipeline_one(c, k, nb, d_ods + (size_t)done * k * k * CDA_SHARE,
-                                         d_eds + (size_t)done * w * w * CDA_SHARE,
-                                         (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES,
-                                         (uint8_t*)d_dah + (size_t)done * 32, d_status + done, s, (size_t)done * w * w))
-        return rc2;
-      done += nb;
-    }
-    return CDA_OK;
-  }
-  const int nsub = (c->prof || c->nsub <= 1) ? 1 : (int)std::min<uint32_t>((uint32_t)c->nsub, nblocks);
-  if (nsub == 1) return enqueue_pipeline_one(c, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, s, 0);
-  if ((rc = ensure_sub(c))) return rc;
-  if (!dev_ok(c, hipEventRecord(c->fork_ev, s), "hipEventRecord")) return CDA_E_DEVICE;
-  uint32_t done = 0;
-  for (int i = 0; i < nsub; i++) {
-    const uint32_t nb = (nblocks - done) / (uint32_t)(nsub - i);
-    if (!dev_ok(c, hipStreamWaitEvent(c->sub[i], c->fork_ev, 0), "hipStreamWaitEvent")) return CDA_E_DEVICE;
-    rc = enqueue_pipeline_one(c, k, nb, d_ods + (size_t)done * k * k * CDA_SHARE, d_eds + (size_t)done * w * w * CDA_SHARE,
-                              (uint8_t*)d_roots + (size_t)done * 2 * w * CDA_REC_BYTES, (uint8_t*)d_dah + (size_t)done * 32,
-                              d_status + done, c->sub[i], (size_t)done * w * w);
-    if (rc) return rc;
-    if (!dev_ok(c, hipEventRecord(c->join_ev[i], c->sub[i]), "hipEventRecord") ||
-        !dev_ok(c, hipStreamWaitEvent(s, c->join_ev[i], 0), "hipStreamWaitEvent"))
-      return CDA_E_DEVICE;
-    done += nb;
-  }
-  return CDA_OK;
+  if ((rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s))) return rc;
+  return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, 0);
 }
 
 // 96-B records -> packed 90-B nodes
@@ -323,12 +263,19 @@ int map_status(uint64_t st, int block, cda_err_info* err) {
 extern "C" {
 
 int cda_init(int device, cda_ctx** out) {
+  CDA_API_TRY
   if (!out) return CDA_E_ARG;
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return CDA_E_DEVICE;
   if (hipSetDevice(device) != hipSuccess) return CDA_E_DEVICE;
   cda_ctx* c = new cda_ctx();
+  struct Owner {  // releases a half-built context on every failure path (including an exception)
+    cda_ctx* c;
+    ~Owner() {
+      if (c) cda_free(c);
+    }
+  } own{c};
   c->device = device;
   const char* fail = nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) fail = "stream";
@@ -337,13 +284,8 @@ int cda_init(int device, cda_ctx** out) {
   else if (rs_decode_init_device_tables(device)) fail = "decode tables";
   if (fail) {
     fprintf(stderr, "cda_init: %s initialisation failed: %s\n", fail, hipGetErrorString(hipGetLastError()));
-    delete c;
     return CDA_E_DEVICE;
   }
-  if (const char* e = getenv("CDA_STREAMS")) c->nsub = std::max(1, std::min(cda_ctx::kMaxSub, atoi(e)));
-  if (const char* e = getenv("CDA_PIPELINE")) c->pipe_chunks = std::max(1, std::min(64, atoi(e)));
-  if (const char* e = getenv("CDA_CHUNK")) c->chunk_blocks = std::max(0, atoi(e));
-  if (const char* e = getenv("CDA_FUSED")) c->fused = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_OVERLAP")) c->repair_overlap = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
@@ -355,19 +297,18 @@ int cda_init(int device, cda_ctx** out) {
             hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) == hipSuccess;
-  for (int i = 0; i < cda_ctx::kMaxSub && ok; i++)
+  for (int i = 0; i < cda_ctx::kJoin && ok; i++)
     ok = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
-  if (!ok) {
-    delete c;
-    return CDA_E_DEVICE;
-  }
+  if (!ok) return CDA_E_DEVICE;
+  own.c = nullptr;
   *out = c;
   return CDA_OK;
+  CDA_API_CATCH(nullptr)
 }
 
 void cda_free(cda_ctx* c) {
   if (!c) return;
-  {
+  try {
     Lock l(c);
     (void)hipStreamSynchronize(c->stream);
     flush_profile(c);
@@ -376,17 +317,16 @@ void cda_free(cda_ctx* c) {
       if (b->p) (void)hipFree(b->p);
     if (c->rstage.p) (void)hipHostFree(c->rstage.p);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    for (int i = 0; i < cda_ctx::kMaxSub; i++) {
-      if (c->sub[i]) (void)hipStreamDestroy(c->sub[i]);
+    for (int i = 0; i < cda_ctx::kJoin; i++)
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
-    }
     free_pipeline(c);
     free_staging(c);
     if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
     if (c->sync_ev) (void)hipEventDestroy(c->sync_ev);
-    (void)hipStreamDestroy(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  } catch (...) {  // nothing may escape the C ABI; the context is released regardless
   }
   delete c;
 }
@@ -408,6 +348,8 @@ const char* cda_strerror(int code) {
     case CDA_E_UNSUPPORTED: return "unsupported configuration";
     case CDA_E_SHARE_VERSION: return "unsupported share version";
     case CDA_E_BLOB_SIZE: return "cannot use zero blob size";
+    case CDA_E_NOMEM: return "out of host memory";
+    case CDA_E_INTERNAL: return "internal error (exception caught at the C ABI)";
     default: return "unknown error";
   }
 }
@@ -421,6 +363,7 @@ int cda_rs_validate_chunk_size(int64_t chunk_size) {
 }
 
 int cda_rs_encode(cda_ctx* c, uint32_t k, uint32_t shard_len, const uint8_t* data, uint8_t* parity) {
+  CDA_API_TRY
   if (!c || !data || !parity || k == 0 || k > 32768) return CDA_E_ARG;
   if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
   Lock l(c);
@@ -448,9 +391,11 @@ int cda_rs_encode(cda_ctx* c, uint32_t k, uint32_t shard_len, const uint8_t* dat
   if (!dev_ok(c, hipStreamSynchronize(c->stream), "sync")) return CDA_E_DEVICE;
   flush_profile(c);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_rs_decode(cda_ctx* c, uint32_t k, uint32_t shard_len, uint8_t* shards, const uint8_t* present) {
+  CDA_API_TRY
   if (!c || !shards || !present || k == 0 || k > 32768) return CDA_E_ARG;
   if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
   uint32_t np = 0;
@@ -483,10 +428,12 @@ int cda_rs_decode(cda_ctx* c, uint32_t k, uint32_t shard_len, uint8_t* shards, c
     return CDA_E_DEVICE;
   flush_profile(c);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds, void* d_roots,
                              void* d_dah, void* d_status, void* stream) {
+  CDA_API_TRY
   if (!c || !d_ods || !d_eds || !d_roots || !d_dah || !d_status || nblocks == 0) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
   if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
@@ -494,10 +441,12 @@ int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const voi
   DevLock l(c, s);
   return enqueue_pipeline(c, k, nblocks, (const uint8_t*)d_ods, (uint8_t*)d_eds, d_roots, d_dah,
                           (unsigned long long*)d_status, s);
+  CDA_API_CATCH(c)
 }
 
 int cda_rs_encode_device(cda_ctx* c, uint32_t k, uint32_t shard_len, uint32_t ncw, const void* d_src, int64_t src_cw,
                          int64_t src_sh, void* d_dst, int64_t dst_cw, int64_t dst_sh, void* stream) {
+  CDA_API_TRY
   if (!c || !d_src || !d_dst || k == 0 || k > 32768) return CDA_E_ARG;
   if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
   if (ncw == 0) return CDA_OK;
@@ -518,11 +467,13 @@ int cda_rs_encode_device(cda_ctx* c, uint32_t k, uint32_t shard_len, uint32_t nc
   const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
   if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_nmt_roots_device(cda_ctx* c, uint32_t k, const void* d_eds, uint32_t axis, uint32_t first_index,
                          uint32_t naxes, uint32_t leaf_off, uint32_t nleaves, void* d_roots, void* d_status,
                          void* stream) {
+  CDA_API_TRY
   if (!c || !d_eds || !d_roots || !d_status || (axis != CDA_AXIS_ROW && axis != CDA_AXIS_COL)) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
   const uint32_t w = 2 * k;
@@ -541,9 +492,11 @@ int cda_nmt_roots_device(cda_ctx* c, uint32_t k, const void* d_eds, uint32_t axi
                                    (unsigned long long*)d_status, s);
   if (lr) return lr == -2 ? CDA_E_ARG : CDA_E_DEVICE;
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_nmt_fold_device(cda_ctx* c, uint32_t ntrees, uint32_t n, const void* d_nodes, void* d_roots, void* stream) {
+  CDA_API_TRY
   if (!c || !d_nodes || !d_roots || !is_pow2(n)) return CDA_E_ARG;
   if (ntrees == 0) return CDA_OK;
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
@@ -556,9 +509,11 @@ int cda_nmt_fold_device(cda_ctx* c, uint32_t ntrees, uint32_t n, const void* d_n
   if (!dev_ok(c, hipMemcpyAsync(c->leaf.p, d_nodes, bytes, hipMemcpyDeviceToDevice, s), "D2D")) return CDA_E_DEVICE;
   ProfScope ps(c, "nmt_fold", s);
   return launch_nmt_fold(c->leaf.p, c->scratch.p, d_roots, (int)ntrees, ilog2i(n), s) ? CDA_E_DEVICE : CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_dah_device(cda_ctx* c, uint32_t n_total, const void* d_roots, void* d_dah, void* stream) {
+  CDA_API_TRY
   if (!c || !d_roots || !d_dah || n_total == 0) return CDA_E_ARG;
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
   DevLock l(c, s);
@@ -566,10 +521,12 @@ int cda_dah_device(cda_ctx* c, uint32_t n_total, const void* d_roots, void* d_da
   const int lr = launch_dah(d_roots, d_dah, (int)n_total, 1, s);
   if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods, uint8_t* eds_or_null,
                             uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !ods || !row_roots || !col_roots || !dah || nblocks == 0) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
@@ -588,8 +545,7 @@ int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint
   // With the EDS wanted (da.ExtendShares returns it): the EDS is final once the extension has run, so its copy-out
   // runs on the D2H stream beside the tree hashing instead of after it.  The hashing is enqueued first: the
   // pageable copy holds this thread until it is done.
-  const bool overlap = eds_or_null && !c->prof && !c->fused && c->pipe_chunks <= 1 && c->chunk_blocks == 0 &&
-                       c->nsub <= 1;
+  const bool overlap = eds_or_null && !c->prof;
   if (overlap) {
     const size_t cells = (size_t)nblocks * w * w;
     if ((rc = ensure_pipeline(c)) || (rc = ensure(c, c->leaf, cells * CDA_REC_BYTES)) ||
@@ -628,10 +584,12 @@ int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint
   for (uint32_t b = 0; b < nblocks; b++)
     if ((rc = map_status(st[b], (int)b, err))) return rc;
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_extend_commit(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares, uint8_t* eds_or_null,
                       uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !shares || !row_roots || !col_roots || !dah) return CDA_E_ARG;
   // da.ExtendShares: power-of-two check (data_availability_header.go:67-69)
@@ -642,10 +600,12 @@ int cda_extend_commit(cda_ctx* c, uint32_t count, uint32_t share_len, const uint
   if (cda_rs_validate_chunk_size(share_len)) return CDA_E_SHARD_SIZE;
   if (share_len != CDA_SHARE) return CDA_E_UNSUPPORTED;
   return cda_extend_commit_batch(c, k, 1, shares, eds_or_null, row_roots, col_roots, dah, err);
+  CDA_API_CATCH(c)
 }
 
 int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                    cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !eds || !row_roots || !col_roots || !dah) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
@@ -687,9 +647,11 @@ int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_root
   pack_roots(recs.data(), w, row_roots);
   pack_roots(recs.data() + (size_t)w * CDA_REC_BYTES, w, col_roots);
   return map_status(st, 0, err);
+  CDA_API_CATCH(c)
 }
 
 int cda_dah_hash(cda_ctx* c, uint32_t n, const uint8_t* row_roots, const uint8_t* col_roots, uint8_t* dah) {
+  CDA_API_TRY
   if (!c || !dah) return CDA_E_ARG;
   if (n == 0) {  // merkle.HashFromByteSlices(nil) = SHA256("")
     static const uint8_t kEmpty[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
@@ -722,10 +684,12 @@ int cda_dah_hash(cda_ctx* c, uint32_t n, const uint8_t* row_roots, const uint8_t
     return CDA_E_DEVICE;
   flush_profile(c);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uint32_t n, uint32_t leaf_len,
                       const uint8_t* leaves, uint8_t* root, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !root || (n && !leaves) || square_size == 0) return CDA_E_ARG;
   // ErasuredNamespacedMerkleTree.Push checks (nmt_wrapper.go:94-99) happen leaf by leaf in the
@@ -783,24 +747,30 @@ int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uin
   if (past) return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, (int)push_limit, -1), CDA_E_PUSH_PAST;
   memcpy(root, rec, CDA_NODE_SIZE);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_profile_enable(cda_ctx* c, int enable) {
+  CDA_API_TRY
   if (!c) return CDA_E_ARG;
   Lock l(c);
   c->prof = enable != 0;
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_profile_reset(cda_ctx* c) {
+  CDA_API_TRY
   if (!c) return CDA_E_ARG;
   Lock l(c);
   flush_profile(c);
   c->prof_acc.clear();
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_profile_read(cda_ctx* c, char* names_buf, size_t names_cap, double* total_ms, int64_t* launches, int cap) {
+  CDA_API_TRY
   if (!c) return CDA_E_ARG;
   Lock l(c);
   flush_profile(c);
@@ -818,6 +788,7 @@ int cda_profile_read(cda_ctx* c, char* names_buf, size_t names_cap, double* tota
     i++;
   }
   return i;
+  CDA_API_CATCH(c)
 }
 
 }  // extern "C"

@@ -130,8 +130,31 @@ int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods
   auto slot_dah = [&](uint32_t i) { return (uint8_t*)c->dah.p + (size_t)(i % S) * C * 32; };
   auto slot_st = [&](uint32_t i) { return (uint8_t*)c->status.p + (size_t)(i % S) * C * 8; };
   const int dev = c->device;
+  // helpers: a failed start of the second (or an exception below) aborts the first and joins it, then the
+  // streams drain before the caller's buffers are released
+  std::thread h2d, d2h;
+  auto stop = [&] {
+    pr.fail();
+    if (h2d.joinable()) h2d.join();
+    if (d2h.joinable()) d2h.join();
+    (void)hipStreamSynchronize(c->h2d_stream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->d2h_stream);
+  };
+  ThreadJoiner<decltype(stop)> joiner(stop);
+  joiner.ts = {&h2d, &d2h};
+  // a helper's own exception (e.g. std::system_error from its mutex) becomes this call's error code
+  auto guarded = [&](auto body) {
+    return [&, body] {
+      try {
+        body();
+      } catch (...) {
+        fail(api_exception(c), nullptr);
+      }
+    };
+  };
 
-  std::thread h2d([&] {
+  h2d = std::thread(guarded([&] {
     (void)hipSetDevice(dev);
     for (uint32_t i = 0; i < nchunks; i++) {
       const int j = (int)(i % S);
@@ -145,8 +168,9 @@ int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods
         return fail(CDA_E_DEVICE, "H2D");
       pr.bump(&Progress::h2d);
     }
-  });
-  std::thread d2h([&] {
+  }));
+  fault_point("thread");
+  d2h = std::thread(guarded([&] {
     (void)hipSetDevice(dev);
     for (uint32_t i = 0; i < nchunks; i++) {
       const int j = (int)(i % S);
@@ -165,7 +189,7 @@ int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods
         return fail(CDA_E_DEVICE, "D2H");
       pr.bump(&Progress::d2h);
     }
-  });
+  }));
   for (uint32_t i = 0; i < nchunks; i++) {
     const int j = (int)(i % S);
     if (!pr.wait_for(&Progress::h2d, i + 1)) break;
@@ -216,18 +240,22 @@ int batch_pipelined(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* ods
 extern "C" {
 
 int cda_host_alloc(cda_ctx* c, size_t bytes, void** out) {
+  CDA_API_TRY
   if (!c || !out) return CDA_E_ARG;
   *out = nullptr;
   Lock l(c);
   if (!dev_ok(c, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault), "hipHostMalloc")) return CDA_E_DEVICE;
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_host_free(cda_ctx* c, void* p) {
+  CDA_API_TRY
   if (!c) return CDA_E_ARG;
   if (!p) return CDA_OK;
   Lock l(c);
   return dev_ok(c, hipHostFree(p), "hipHostFree") ? CDA_OK : CDA_E_DEVICE;
+  CDA_API_CATCH(c)
 }
 
 // ---- multi-device batch ----------------------------------------------------------------------
@@ -237,24 +265,31 @@ struct cda_multi {
 };
 
 int cda_multi_init(uint32_t device_mask, cda_multi** out) {
+  CDA_API_TRY
   if (!out) return CDA_E_ARG;
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CDA_E_DEVICE;
   if (device_mask == 0) device_mask = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
   cda_multi* m = new cda_multi();
+  struct Owner {
+    cda_multi* m;
+    ~Owner() {
+      if (m) cda_multi_free(m);
+    }
+  } own{m};
   for (int d = 0; d < 32; d++) {
     if (!(device_mask & (1u << d))) continue;
     cda_ctx* c = nullptr;
-    if (d >= n || cda_init(d, &c) != CDA_OK) {
-      cda_multi_free(m);
-      return CDA_E_DEVICE;
-    }
+    if (d >= n || cda_init(d, &c) != CDA_OK) return CDA_E_DEVICE;
+    m->ctx.reserve(m->ctx.size() + 1);
     m->ctx.push_back(c);
     m->devices.push_back(d);
   }
+  own.m = nullptr;
   *out = m;
   return CDA_OK;
+  CDA_API_CATCH(nullptr)
 }
 
 void cda_multi_free(cda_multi* m) {
@@ -265,6 +300,10 @@ void cda_multi_free(cda_multi* m) {
 
 int cda_multi_device_count(const cda_multi* m) { return m ? (int)m->ctx.size() : 0; }
 
+int cda_multi_device(const cda_multi* m, int i) {
+  return (m && i >= 0 && i < (int)m->devices.size()) ? m->devices[i] : -1;
+}
+
 cda_ctx* cda_multi_context(cda_multi* m, int i) {
   return (m && i >= 0 && i < (int)m->ctx.size()) ? m->ctx[i] : nullptr;
 }
@@ -272,6 +311,7 @@ cda_ctx* cda_multi_context(cda_multi* m, int i) {
 int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, const uint8_t* ods,
                                   uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                                   cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!m || m->ctx.empty() || !ods || !row_roots || !col_roots || !dah || nblocks == 0) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
@@ -283,6 +323,14 @@ int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, co
   std::vector<int> rcs(G, CDA_OK);
   std::vector<cda_err_info> errs(G);
   std::vector<std::thread> th;
+  th.reserve(G);
+  struct JoinAll {
+    std::vector<std::thread>& v;
+    ~JoinAll() {
+      for (auto& t : v)
+        if (t.joinable()) t.join();
+    }
+  } join_all{th};
   uint32_t done = 0;
   for (uint32_t g = 0; g < G; g++) {  // contiguous block ranges, no collective
     const uint32_t nb = (nblocks - done) / (G - g);
@@ -291,10 +339,15 @@ int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, co
     if (nb == 0) continue;
     th.emplace_back([&, g, nb, b0] {
       cda_ctx* c = m->ctx[g];
-      Lock l(c);
-      rcs[g] = batch_pipelined(c, k, nb, ods + (size_t)b0 * ods_blk, eds_or_null ? eds_or_null + (size_t)b0 * eds_blk : nullptr,
-                               row_roots + (size_t)b0 * root_blk, col_roots + (size_t)b0 * root_blk, dah + (size_t)b0 * 32,
-                               &errs[g], (int)b0);
+      try {
+        Lock l(c);
+        rcs[g] = batch_pipelined(c, k, nb, ods + (size_t)b0 * ods_blk,
+                                 eds_or_null ? eds_or_null + (size_t)b0 * eds_blk : nullptr,
+                                 row_roots + (size_t)b0 * root_blk, col_roots + (size_t)b0 * root_blk,
+                                 dah + (size_t)b0 * 32, &errs[g], (int)b0);
+      } catch (...) {
+        rcs[g] = api_exception(c);
+      }
     });
   }
   for (auto& t : th) t.join();
@@ -306,6 +359,7 @@ int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, co
       return rcs[g];
     }
   return CDA_OK;
+  CDA_API_CATCH(nullptr)
 }
 
 }  // extern "C"

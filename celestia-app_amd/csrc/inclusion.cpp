@@ -93,6 +93,7 @@ extern "C" {
 int cda_blob_commitments(cda_ctx* c, uint32_t nblobs, const uint8_t* namespaces, const uint8_t* data,
                          const uint64_t* offsets, const uint8_t* share_versions, uint32_t subtree_root_threshold,
                          uint8_t* commitments, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || subtree_root_threshold == 0) return CDA_E_ARG;
   if (nblobs == 0) return CDA_OK;
@@ -176,10 +177,12 @@ int cda_blob_commitments(cda_ctx* c, uint32_t nblobs, const uint8_t* namespaces,
     return CDA_E_DEVICE;
   flush_profile(c);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_merkle_roots(cda_ctx* c, uint32_t nsets, const uint32_t* set_offsets, const uint8_t* items, uint32_t item_len,
                      uint8_t* roots) {
+  CDA_API_TRY
   if (!c) return CDA_E_ARG;
   if (item_len != CDA_NODE_SIZE) return CDA_E_UNSUPPORTED;
   if (nsets == 0) return CDA_OK;
@@ -216,11 +219,13 @@ int cda_merkle_roots(cda_ctx* c, uint32_t nsets, const uint32_t* set_offsets, co
     return CDA_E_DEVICE;
   flush_profile(c);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares, uint8_t* eds_or_null,
                             uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, uint8_t* row_nodes,
                             uint8_t* col_nodes, uint8_t* dah_nodes, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !shares || !row_roots || !col_roots || !dah) return CDA_E_ARG;
   uint32_t k = 0;
@@ -319,12 +324,14 @@ int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, cons
     }
   }
   return map_status(st, 0, err);
+  CDA_API_CATCH(c)
 }
 
 int cda_share_inclusion_proof(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares, uint32_t start,
                               uint32_t end, cda_share_proof_info* info, uint8_t* row_roots, uint8_t* leaf_hashes,
                               uint8_t* aunts, int32_t* nmt_start, int32_t* nmt_end, int32_t* nmt_count,
                               uint8_t* nmt_nodes, uint8_t* data_root, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !shares || !info || !row_roots || !leaf_hashes || !aunts || !nmt_start || !nmt_end || !nmt_count ||
       !nmt_nodes)
@@ -373,6 +380,7 @@ int cda_share_inclusion_proof(cda_ctx* c, uint32_t count, uint32_t share_len, co
   }
   if (data_root) memcpy(data_root, root, 32);
   return CDA_OK;
+  CDA_API_CATCH(c)
 }
 
 }  // extern "C"

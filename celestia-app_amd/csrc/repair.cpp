@@ -176,15 +176,23 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   std::thread h2d;
   if (eds)
     h2d = std::thread([&] {
-      (void)hipSetDevice(c->device);
-      h2d_ok = staged_h2d(c, d_eds, eds, eds_b, s) == CDA_OK;
+      try {
+        (void)hipSetDevice(c->device);
+        h2d_ok = staged_h2d(c, d_eds, eds, eds_b, s) == CDA_OK;
+      } catch (...) {  // nothing may escape a helper thread (std::terminate)
+        (void)api_exception(c);
+        h2d_ok = false;
+      }
     });
-  struct Joiner {
+  struct Joiner {  // an early return or exception: the upload finishes before the caller's buffer is released
     std::thread& t;
+    hipStream_t s;
     ~Joiner() {
-      if (t.joinable()) t.join();
+      if (!t.joinable()) return;
+      t.join();
+      (void)hipStreamSynchronize(s);
     }
-  } joiner{h2d};
+  } joiner{h2d, s};
   RepairTrace tr;
   tr.mark("setup");
   Presence P;
@@ -297,6 +305,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     ((int*)(h + o_all))[w + i] = enc_axis(CDA_AXIS_COL, i);
   }
   tr.mark("plan");
+  fault_point("thread");
   if (h2d.joinable()) h2d.join();
   tr.mark("h2d_wait");
   if (!h2d_ok) {
@@ -477,28 +486,33 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   tr.mark("enqueue");
   if (early)  // rows whose last writer has run go back on their own stream (pageable: from a helper thread)
     early_d2h = std::thread([&] {
-      (void)hipSetDevice(c->device);
-      hipStream_t d2h = c->d2h_stream;
-      const size_t row_b = W * CDA_SHARE;
-      for (size_t b = 0; b < nbat && !early_failed; b++) {
-        if (!bev[b]) continue;
-        if (hipEventSynchronize(bev[b]) != hipSuccess) {
-          early_failed = true;
-          break;
-        }
-        for (int r = 0; r < w;) {  // runs of consecutive rows finished by batch b
-          if (blast[r] != (int)b) {
-            r++;
-            continue;
-          }
-          int r1 = r;
-          while (r1 < w && blast[r1] == (int)b) r1++;
-          if (staged_d2h(c, eds + r * row_b, d_eds + r * row_b, (size_t)(r1 - r) * row_b, d2h) != CDA_OK)
+      try {
+        (void)hipSetDevice(c->device);
+        hipStream_t d2h = c->d2h_stream;
+        const size_t row_b = W * CDA_SHARE;
+        for (size_t b = 0; b < nbat && !early_failed; b++) {
+          if (!bev[b]) continue;
+          if (hipEventSynchronize(bev[b]) != hipSuccess) {
             early_failed = true;
-          r = r1;
+            break;
+          }
+          for (int r = 0; r < w;) {  // runs of consecutive rows finished by batch b
+            if (blast[r] != (int)b) {
+              r++;
+              continue;
+            }
+            int r1 = r;
+            while (r1 < w && blast[r1] == (int)b) r1++;
+            if (staged_d2h(c, eds + r * row_b, d_eds + r * row_b, (size_t)(r1 - r) * row_b, d2h) != CDA_OK)
+              early_failed = true;
+            r = r1;
+          }
         }
+        if (hipStreamSynchronize(d2h) != hipSuccess) early_failed = true;
+      } catch (...) {
+        (void)api_exception(c);
+        early_failed = true;
       }
-      if (hipStreamSynchronize(d2h) != hipSuccess) early_failed = true;
     });
   if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
   tr.mark("gpu_wait");
@@ -575,22 +589,26 @@ extern "C" {
 
 int cda_repair(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
   if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   Lock l(c);
   return repair_impl(c, k, eds, nullptr, present, row_roots, col_roots, err, c->stream);
+  CDA_API_CATCH(c)
 }
 
 int cda_repair_device(cda_ctx* c, uint32_t k, void* d_eds, uint8_t* present, const uint8_t* row_roots,
                       const uint8_t* col_roots, cda_err_info* err, void* stream) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !d_eds || !present || !row_roots || !col_roots) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
   if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   DevLock l(c, (hipStream_t)stream);
   return repair_impl(c, k, nullptr, (uint8_t*)d_eds, present, row_roots, col_roots, err, (hipStream_t)stream);
+  CDA_API_CATCH(c)
 }
 
 }  // extern "C"

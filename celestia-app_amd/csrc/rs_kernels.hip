@@ -30,7 +30,6 @@
 #include "cda_internal.h"
 #include "gf8_const.h"
 #include "gf_slice.h"
-#include "nmt_dev.h"
 
 namespace cda {
 
@@ -511,144 +510,7 @@ __global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegA
   rs_g2_body<L>(a, blockIdx.x, xbuf);
 }
 
-// ===========================================================================
-// Extension fused with leaf hashing (the block path, k = 16..128).
-//
-// The RS kernels alone are HBM- and VALU-bound at once and run their load and compute phases
-// largely in lockstep; the leaf hashing is VALU-bound (SHA-256) with little memory traffic.  Fusing
-// them gives every workgroup a short memory phase (its codewords) and a long VALU phase (9 SHA-256
-// compressions per cell), so the two workgroups of a CU overlap one's HBM traffic with the other's
-// hashing, and the separate leaf kernel's re-read of the EDS disappears.
-//   rows kernel: 2 ODS rows -> Q0 copy + Q1 (rsmt2d Q1 = Enc(Q0 rows)), then hashes those 2 x 2k cells
-//                (Q0 bytes and push-order neighbours from the ODS, Q1 from what it just stored);
-//   cols kernel: 2 x 2 columns -> Q2|Q3 (Q3 = Enc(Q2 rows) = Enc_col(Q1), linear code), then hashes
-//                those 4 x k bottom cells (all parity: namespace 0xFF x 29, no order check).
-// One cell per thread in the hashing phase (blockDim = 4k).  The workgroup barrier orders its own
-// global stores before its loads of the same cells (workgroup-scope release/acquire).
-// Measured (MI355X, k=128, B=128): rows+leaf 2.03 ms + cols+leaf 2.47 ms against 0.665 + 1.114 + 2.76 ms
-// for the three separate kernels -- no net gain: the RS body needs 128 VGPRs (4 waves per SIMD), so
-// when half the waves of a CU wait on memory or barriers the other half cannot keep the VALU busy
-// (waitcnt/barrier 0.30 of wave time vs 0.05 in the leaf kernel; a per-CU phase offset of the
-// second workgroup changed nothing).  Kept behind CDA_FUSED=1; the default is the separate kernels.
-// ===========================================================================
-struct LeafArgs {
-  const uint8_t* ods;          // [blk][k][k][512]
-  const uint8_t* eds;          // [blk][2k][2k][512]
-  uint4* nodes;                // leaf records [blk][2k][2k] x 96 B
-  unsigned long long* status;  // per block: first push-order violation (atomicMin), all-ones = ok
-};
-
-template <int L>
-__global__ void __launch_bounds__(64 << (L - 4), 4) rs_rows_leaf_kernel(Rs8RegArgs a, LeafArgs h) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
-  constexpr int K = 1 << L, W = 2 * K, LW = L + 1;
-  rs_g2_body<L>(a, blockIdx.x, xbuf);
-  __syncthreads();
-  const int grp = blockIdx.x % a.groups_per_blk, blk = blockIdx.x / a.groups_per_blk;
-  const int t = threadIdx.x;
-  const int r = 2 * grp + (t >> LW), c = t & (W - 1);
-  const size_t gid = ((size_t)blk << (2 * LW)) + ((size_t)r << LW) + (size_t)c;
-  uint4* out = h.nodes + gid * 6;
-  if (c < K) {  // Q0 cell: the ODS share itself; push order against its Q0 right / lower neighbours
-    const uint8_t* q = h.ods + (((size_t)blk * K + r) * K + c) * CDA_SHARE;
-    const uint4* sh = reinterpret_cast<const uint4*>(q);
-    uint32_t A[16];
-    load16(sh, A);
-    if (c + 1 < K) {
-      const uint4* p = reinterpret_cast<const uint4*>(q + CDA_SHARE);
-      const uint4 v0 = p[0], v1 = p[1];
-      const uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (ns_cmp(nb, A) < 0)
-        atomicMin(h.status + blk, ((unsigned long long)CDA_AXIS_ROW << 40) | ((unsigned long long)r << 20) | (c + 1));
-    }
-    if (r + 1 < K) {
-      const uint4* p = reinterpret_cast<const uint4*>(q + (size_t)K * CDA_SHARE);
-      const uint4 v0 = p[0], v1 = p[1];
-      const uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (ns_cmp(nb, A) < 0)
-        atomicMin(h.status + blk, ((unsigned long long)CDA_AXIS_COL << 40) | ((unsigned long long)c << 20) | (r + 1));
-    }
-    leaf_record(sh, A, true, out);
-  } else {  // Q1 parity cell this workgroup just stored
-    const uint4* sh = reinterpret_cast<const uint4*>(h.eds + gid * CDA_SHARE);
-    uint32_t A[16];
-    load16(sh, A);
-    leaf_record(sh, A, false, out);
-  }
-}
-
-template <int L>
-__global__ void __launch_bounds__(64 << (L - 4), 4) rs_cols_leaf_kernel(Rs8RegArgs a, LeafArgs h) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
-  constexpr int K = 1 << L, LW = L + 1;
-  // two column pairs per workgroup (groups_per_blk counts pairs; it is even for K >= 16)
-  const int g0 = 2 * (int)blockIdx.x;
-#pragma unroll 1
-  for (int pass = 0; pass < 2; pass++) {
-    rs_g2_body<L>(a, g0 + pass, xbuf);
-    __syncthreads();
-  }
-  const int grp = g0 % a.groups_per_blk, blk = g0 / a.groups_per_blk;
-  const int t = threadIdx.x;
-  const int c = 2 * grp + (t & 3), r = K + (t >> 2);  // 4 adjacent columns per row: 2 KiB runs
-  const size_t gid = ((size_t)blk << (2 * LW)) + ((size_t)r << LW) + (size_t)c;
-  const uint4* sh = reinterpret_cast<const uint4*>(h.eds + gid * CDA_SHARE);
-  uint32_t A[16];
-  load16(sh, A);
-  leaf_record(sh, A, false, h.nodes + gid * 6);
-}
-
 static Rs8RegArgs reg_args(const RsJob& j);
-
-static int fused_L(const RsJob& j) {
-  int L = 0;
-  while ((1 << L) < j.k) L++;
-  if ((1 << L) != j.k || L < 4 || L > 7 || j.shard_len != CDA_SHARE || j.cw_per_blk % 4) return -1;
-  return L;
-}
-
-bool rs_leaf_fusable(int k) {
-  RsJob j{};
-  j.k = k;
-  j.shard_len = CDA_SHARE;
-  j.cw_per_blk = 2 * k;
-  return fused_L(j) >= 0;
-}
-
-int launch_rs_rows_leaf(const RsJob& rows, const uint8_t* d_ods, const uint8_t* d_eds, void* d_nodes,
-                        unsigned long long* d_status, hipStream_t s) {
-  const int L = fused_L(rows);
-  if (L < 0 || rows.cw_per_blk != rows.k) return -2;
-  const Rs8RegArgs ra = reg_args(rows);
-  const LeafArgs h{d_ods, d_eds, (uint4*)d_nodes, d_status};
-  const size_t lds = L > 4 ? (size_t)(1 << L) * 32 * 16 : 0;
-  const unsigned grid = (unsigned)((long long)rows.nblk * ra.groups_per_blk);
-  const dim3 block(64 << (L - 4));
-  switch (L) {
-    case 4: hipLaunchKernelGGL(rs_rows_leaf_kernel<4>, dim3(grid), block, lds, s, ra, h); break;
-    case 5: hipLaunchKernelGGL(rs_rows_leaf_kernel<5>, dim3(grid), block, lds, s, ra, h); break;
-    case 6: hipLaunchKernelGGL(rs_rows_leaf_kernel<6>, dim3(grid), block, lds, s, ra, h); break;
-    default: hipLaunchKernelGGL(rs_rows_leaf_kernel<7>, dim3(grid), block, lds, s, ra, h); break;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_rs_cols_leaf(const RsJob& cols, const uint8_t* d_eds, void* d_nodes, hipStream_t s) {
-  const int L = fused_L(cols);
-  if (L < 0 || cols.cw_per_blk != 2 * cols.k) return -2;
-  const Rs8RegArgs ca = reg_args(cols);
-  const LeafArgs h{nullptr, d_eds, (uint4*)d_nodes, nullptr};
-  const size_t lds = L > 4 ? (size_t)(1 << L) * 32 * 16 : 0;
-  const unsigned grid = (unsigned)((long long)cols.nblk * ca.groups_per_blk / 2);
-  const dim3 block(64 << (L - 4));
-  switch (L) {
-    case 4: hipLaunchKernelGGL(rs_cols_leaf_kernel<4>, dim3(grid), block, lds, s, ca, h); break;
-    case 5: hipLaunchKernelGGL(rs_cols_leaf_kernel<5>, dim3(grid), block, lds, s, ca, h); break;
-    case 6: hipLaunchKernelGGL(rs_cols_leaf_kernel<6>, dim3(grid), block, lds, s, ca, h); break;
-    default: hipLaunchKernelGGL(rs_cols_leaf_kernel<7>, dim3(grid), block, lds, s, ca, h); break;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 int rs_init_device_tables(int device) {
   (void)device;
@@ -675,12 +537,8 @@ int rs_init_device_tables(int device) {
   if (hipFuncSetAttribute((const void*)rs_encode8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
       hipSuccess)
     return -1;
-  const void* g2k[12] = {(const void*)rs_encode8_g2_kernel<4>, (const void*)rs_encode8_g2_kernel<5>,
-                         (const void*)rs_encode8_g2_kernel<6>, (const void*)rs_encode8_g2_kernel<7>,
-                         (const void*)rs_rows_leaf_kernel<4>,  (const void*)rs_rows_leaf_kernel<5>,
-                         (const void*)rs_rows_leaf_kernel<6>,  (const void*)rs_rows_leaf_kernel<7>,
-                         (const void*)rs_cols_leaf_kernel<4>,  (const void*)rs_cols_leaf_kernel<5>,
-                         (const void*)rs_cols_leaf_kernel<6>,  (const void*)rs_cols_leaf_kernel<7>};
+  const void* g2k[4] = {(const void*)rs_encode8_g2_kernel<4>, (const void*)rs_encode8_g2_kernel<5>,
+                        (const void*)rs_encode8_g2_kernel<6>, (const void*)rs_encode8_g2_kernel<7>};
   for (auto f : g2k)
     if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) != hipSuccess) return -1;
 

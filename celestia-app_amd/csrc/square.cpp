@@ -45,6 +45,7 @@ extern "C" {
 
 int cda_build_ods_device(cda_ctx* c, uint32_t k, uint32_t nseg, const cda_share_segment* segs, const uint8_t* data,
                          uint64_t data_len, const uint32_t* reserved, uint32_t nreserved, void* d_ods, void* stream) {
+  CDA_API_TRY
   if (!c || !d_ods || !is_pow2(k) || k > kMaxDeviceK) return CDA_E_ARG;
   if (int rc = check_plan(k, nseg, segs, data_len, nreserved)) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
@@ -61,12 +62,14 @@ int cda_build_ods_device(cda_ctx* c, uint32_t k, uint32_t nseg, const cda_share_
   const int lr = launch_build_ods((const cda_share_segment*)d_plan, (int)nseg, (const uint8_t*)c->payload.p,
                                   (const uint32_t*)(d_plan + seg_b), k * k, d_ods, s);
   return lr == 0 ? CDA_OK : (lr == -2 ? CDA_E_ARG : CDA_E_DEVICE);
+  CDA_API_CATCH(c)
 }
 
 int cda_construct_extend_commit(cda_ctx* c, uint32_t k, uint32_t nseg, const cda_share_segment* segs,
                                 const uint8_t* data, uint64_t data_len, const uint32_t* reserved, uint32_t nreserved,
                                 uint8_t* ods_or_null, uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots,
                                 uint8_t* dah, cda_err_info* err) {
+  CDA_API_TRY
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!c || !row_roots || !col_roots || !dah) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
@@ -98,6 +101,7 @@ int cda_construct_extend_commit(cda_ctx* c, uint32_t k, uint32_t nseg, const cda
   pack_roots(recs.data(), w, row_roots);
   pack_roots(recs.data() + (size_t)w * CDA_REC_BYTES, w, col_roots);
   return map_status(st, 0, err);
+  CDA_API_CATCH(c)
 }
 
 }  // extern "C"

@@ -104,7 +104,13 @@ static int get_stager(cda_ctx* c, Stager*& st) {
     delete s;
     return CDA_E_DEVICE;
   }
-  for (int i = 0; i < Stager::kWorkers; i++) s->th.emplace_back([s, i] { s->worker(i); });
+  try {
+    s->th.reserve(Stager::kWorkers);
+    for (int i = 0; i < Stager::kWorkers; i++) s->th.emplace_back([s, i] { s->worker(i); });
+  } catch (...) {
+    delete s;  // stops and joins the workers already started
+    throw;
+  }
   st = s;
   return CDA_OK;
 }

@@ -68,6 +68,8 @@ const (
 	ErrCodeUnrepairable = int(C.CDA_E_UNREPAIRABLE)
 	ErrCodeByzantine    = int(C.CDA_E_BYZANTINE)
 	ErrCodePushPast     = int(C.CDA_E_PUSH_PAST)
+	ErrCodeNoMem        = int(C.CDA_E_NOMEM)    // std::bad_alloc caught inside libcda
+	ErrCodeInternal     = int(C.CDA_E_INTERNAL) // any other C++ exception caught at the C ABI
 )
 
 func toErr(rc C.int, info *C.cda_err_info) error {
@@ -105,15 +107,28 @@ func (x *Context) Close() {
 }
 
 var (
-	defaultOnce sync.Once
-	defaultCtx  *Context
-	defaultErr  error
+	deviceMu   sync.Mutex
+	deviceCtxs = map[int]*Context{}
 )
 
 // Default returns the process-wide context on device 0 (one process per GPU).
-func Default() (*Context, error) {
-	defaultOnce.Do(func() { defaultCtx, defaultErr = NewContext(0) })
-	return defaultCtx, defaultErr
+func Default() (*Context, error) { return DefaultOn(0) }
+
+// DefaultOn returns the process-wide context of HIP device `device`, created on first use and never closed.  The
+// squares ExtendShares / Multi.ExtendBlocks return keep their codec and tree constructor on these contexts, so a
+// returned *rsmt2d.ExtendedDataSquare stays usable (Repair, re-rooting after SetCell) whatever is closed later.
+func DefaultOn(device int) (*Context, error) {
+	deviceMu.Lock()
+	defer deviceMu.Unlock()
+	if x, ok := deviceCtxs[device]; ok {
+		return x, nil
+	}
+	x, err := NewContext(device)
+	if err != nil {
+		return nil, err
+	}
+	deviceCtxs[device] = x
+	return x, nil
 }
 
 func mustDefault() *Context {

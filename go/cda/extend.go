@@ -58,13 +58,27 @@ func ExtendSharesOn(ctx *Context, s [][]byte) (*rsmt2d.ExtendedDataSquare, error
 	return importWithRoots(ctx, eds, w, n, rows, cols)
 }
 
+// importWithRoots wraps the GPU's EDS as an *rsmt2d.ExtendedDataSquare whose row and column roots are already
+// set: RowRoots / ColRoots run here, before the square is handed out, so the root cache's trees only ever see the
+// imported, unmodified cells.  Any later tree (Repair, or re-rooting after SetCell) is a full Tree that hashes what
+// is pushed to it.
 func importWithRoots(ctx *Context, eds []byte, w, n int, rows, cols []byte) (*rsmt2d.ExtendedDataSquare, error) {
 	cache := &rootCache{}
 	cache.roots[0] = split(rows, w)
 	cache.roots[1] = split(cols, w)
 	cache.used[0] = make([]bool, w)
 	cache.used[1] = make([]bool, w)
-	return rsmt2d.ImportExtendedDataSquare(split(eds, w*w), NewCodecOn(ctx), cache.constructor(ctx, uint64(w/2)))
+	sq, err := rsmt2d.ImportExtendedDataSquare(split(eds, w*w), NewCodecOn(ctx), cache.constructor(ctx, uint64(w/2)))
+	if err != nil {
+		return nil, err
+	}
+	if _, err := sq.RowRoots(); err != nil {
+		return nil, err
+	}
+	if _, err := sq.ColRoots(); err != nil {
+		return nil, err
+	}
+	return sq, nil
 }
 
 // Block is one extended block of a batch: the EDS and the DAH inputs.
@@ -89,7 +103,8 @@ func NewMulti(mask uint32) (*Multi, error) {
 	return &Multi{m: m}, nil
 }
 
-// Close releases every device context.
+// Close releases the handle's device contexts.  Blocks returned by ExtendBlocks do not depend on them: their
+// squares use the process-wide DefaultOn contexts, so they stay valid after Close.
 func (m *Multi) Close() {
 	if m.m != nil {
 		C.cda_multi_free(m.m)
@@ -138,7 +153,13 @@ func (m *Multi) ExtendBlocks(blocks [][][]byte, withEDS bool) ([]Block, error) {
 	if rc != 0 {
 		return nil, toErr(rc, &info)
 	}
-	ctx := &Context{c: C.cda_multi_context(m.m, 0)}
+	var ctx *Context
+	if withEDS { // the squares outlive m: their codec / trees run on the process-wide context of m's first device
+		var err error
+		if ctx, err = DefaultOn(int(C.cda_multi_device(m.m, 0))); err != nil {
+			return nil, err
+		}
+	}
 	out := make([]Block, nb)
 	for b := range out {
 		r := rows[b*w*NodeSize : (b+1)*w*NodeSize]

@@ -8,6 +8,8 @@ package cda
 import "C"
 
 import (
+	"fmt"
+
 	"github.com/celestiaorg/rsmt2d"
 )
 
@@ -15,17 +17,27 @@ import (
 // prerepairSanityCheck + solveCrossword order, the same ErrUnrepairableDataSquare / ErrByzantineData{Axis, Index}
 // outcomes, and on a Byzantine error the square left as repaired as rsmt2d leaves it.  eds is flattened
 // row-major with nil for missing cells; the repaired cells are returned in place of the nils.
+//
+// libcda repairs 512-byte shares (appconsts.ShareSize) and reads and writes exactly w*w*512 bytes, so the shape is
+// checked here before the cgo call: len(eds) == w*w with w = len(rowRoots) == len(colRoots), every non-nil cell
+// ShareSize bytes and every root NodeSize bytes.  A mismatch returns an error (as Codec.Decode returns
+// reedsolomon.ErrShardSize) instead of letting the library write past a Go buffer.
 func Repair(ctx *Context, eds [][]byte, rowRoots, colRoots [][]byte) error {
 	w := len(rowRoots)
-	n := 0
-	for _, c := range eds {
-		if len(c) > 0 {
-			n = len(c)
-			break
+	if w == 0 || w%2 != 0 || len(colRoots) != w || len(eds) != w*w {
+		return fmt.Errorf("cda: Repair needs a %dx%d square and %d roots per axis: got %d cells, %d row and %d column roots",
+			w, w, w, len(eds), len(rowRoots), len(colRoots))
+	}
+	for i, r := range rowRoots {
+		if len(r) != NodeSize || len(colRoots[i]) != NodeSize {
+			return fmt.Errorf("cda: Repair roots must be %d bytes (axis index %d)", NodeSize, i)
 		}
 	}
-	if n == 0 {
-		n = ShareSize
+	const n = ShareSize
+	for i, c := range eds {
+		if c != nil && len(c) != n {
+			return fmt.Errorf("cda: Repair cell %d is %d bytes, want %d (shard sizes must be equal)", i, len(c), n)
+		}
 	}
 	buf := make([]byte, w*w*n)
 	present := make([]byte, w*w)

@@ -87,10 +87,10 @@ func (t *Tree) Root() ([]byte, error) {
 	return root, nil
 }
 
-// rootCache hands out the roots the GPU computed for a whole square, once per axis: the first
-// computeRoots pass of the EDS that ExtendShares returns reads them instead of re-hashing (cda_extend_commit
-// already checked every push order).  A later tree of the same (axis, index) -- rsmt2d builds one only after
-// cells changed, e.g. in Repair -- is a full Tree that hashes what is pushed to it.
+// rootCache hands out the roots the GPU computed for a whole square, once per axis: the computeRoots pass that
+// importWithRoots runs on the freshly imported square (before any caller can change a cell) reads them instead of
+// re-hashing (cda_extend_commit already checked every push order).  Every later tree of the square -- rsmt2d builds
+// one only after cells changed, e.g. in Repair -- is a full Tree that hashes what is pushed to it.
 type rootCache struct {
 	mu    sync.Mutex
 	roots [2][][]byte // [rsmt2d.Row / rsmt2d.Col][index]
@@ -117,7 +117,13 @@ func (t *cachedTree) Push(data []byte) error {
 	return nil
 }
 
-func (t *cachedTree) Root() ([]byte, error) { return append([]byte(nil), t.root...), nil }
+func (t *cachedTree) Root() ([]byte, error) {
+	if t.pushed != 2*t.squareSize { // only a whole-axis computeRoots pass may read the precomputed root
+		return nil, fmt.Errorf("cda: cached root of axis %d requested after %d of %d pushes", t.axisIndex, t.pushed,
+			2*t.squareSize)
+	}
+	return append([]byte(nil), t.root...), nil
+}
 
 func (c *rootCache) constructor(ctx *Context, squareSize uint64) rsmt2d.TreeConstructorFn {
 	return func(axis rsmt2d.Axis, axisIndex uint) rsmt2d.Tree {

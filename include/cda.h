@@ -46,6 +46,10 @@ enum {
   CDA_E_UNSUPPORTED = -12, /* configuration not implemented on the device path */
   CDA_E_SHARE_VERSION = -13, /* x/blob ErrUnsupportedShareVersion (appconsts.SupportedShareVersions = {0}) */
   CDA_E_BLOB_SIZE = -14,     /* x/blob ErrZeroBlobSize: empty blob data (x/blob/types/payforblob.go:230-232) */
+  CDA_E_NOMEM = -15,         /* host allocation failed inside the library (std::bad_alloc caught at the C ABI) */
+  CDA_E_INTERNAL = -16,      /* any other C++ exception caught at the C ABI (e.g. a helper thread failed to start);
+                                no exception ever crosses an entry point (app/process_proposal.go:28-34 recovers
+                                Go panics only) */
 };
 
 enum { CDA_AXIS_ROW = 0, CDA_AXIS_COL = 1 }; /* rsmt2d.Row / rsmt2d.Col */
@@ -124,6 +128,8 @@ void cda_multi_free(cda_multi* m);
 int cda_multi_device_count(const cda_multi* m);
 /* The per-device context i (0-based, in device order) for the single-device entry points. */
 cda_ctx* cda_multi_context(cda_multi* m, int i);
+/* HIP device id of the handle's device i (0-based, in device order), or -1. */
+int cda_multi_device(const cda_multi* m, int i);
 int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, const uint8_t* ods,
                                   uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                                   cda_err_info* err);

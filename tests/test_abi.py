@@ -71,3 +71,19 @@ def test_new_entry_points_reject_null_context_without_gpu():
                                        None, None) == N.E_ARG
     assert N.strerror(N.E_BLOB_SIZE) == "cannot use zero blob size"
     assert N.strerror(N.E_SHARE_VERSION) == "unsupported share version"
+
+
+def test_exception_barrier_without_gpu(monkeypatch):
+    """No C++ exception crosses the C ABI (no abort; app/process_proposal.go:28-34 recovers Go panics
+    only): an exception injected at entry (CDA_FAULT_INJECT=entry throws std::bad_alloc before the body runs) comes
+    back as CDA_E_NOMEM from every kind of entry point, not as std::terminate."""
+    L = cda.lib()
+    monkeypatch.setenv("CDA_FAULT_INJECT", "entry")
+    assert L.cda_merkle_roots(None, 1, None, None, 90, None) == N.E_NOMEM
+    assert L.cda_repair(None, 8, None, None, None, None, None) == N.E_NOMEM
+    assert L.cda_extend_commit(None, 4, 512, None, None, None, None, None, None) == N.E_NOMEM
+    assert L.cda_multi_extend_commit_batch(None, 8, 1, None, None, None, None, None, None) == N.E_NOMEM
+    monkeypatch.delenv("CDA_FAULT_INJECT")
+    assert L.cda_merkle_roots(None, 1, None, None, 90, None) == N.E_ARG
+    assert N.strerror(N.E_NOMEM) == "out of host memory"
+    assert N.strerror(N.E_INTERNAL).startswith("internal error")
