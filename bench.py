@@ -43,18 +43,12 @@ def kernel_step_bytes(name, k, B):
     NMT levels: read 2 child nodes, write 1 (90 B each); dah: read 4k roots.
     """
     w, S, N = 2 * k, 512, 90
-    if name == "rs_rows_leaf":  # read ODS, write Q0 copy + Q1, top-half leaf nodes
-        return B * (3 * k * k * S + k * w * N)
-    if name == "rs_cols_leaf":  # read the top half, write the bottom half and its leaf nodes
-        return B * (2 * w * k * S + k * w * N)
     if name.endswith("_rows"):
         return B * 3 * k * k * S
     if name.endswith("_cols"):
         return B * 2 * w * k * S
     if name == "leaf_hash":
         return B * w * w * (S + N)
-    if name == "nmt_level1":
-        return B * 2 * w * (w // 2) * 3 * N
     if name == "nmt_levels_1":  # levels 1-2 in one launch: read the leaves, write levels 1 and 2
         return B * 2 * w * ((w // 2) * 2 * N + (w // 2) * N + (w // 4) * N)
     if name == "nmt_levels":  # levels 3..log2(w): read level 2, write every later level
@@ -63,14 +57,66 @@ def kernel_step_bytes(name, k, B):
             tot += 2 * w * (n // 2) * N
             n //= 2
         return B * tot
-    if name == "nmt_level":  # levels 2..log2(w)
-        n, tot = w // 2, 0
-        while n > 1:
-            tot += 2 * w * (n // 2) * 3 * N
-            n //= 2
-        return B * tot
     if name == "dah":
         return B * (2 * w * N + 32)
+    return None
+
+
+# What bounds each kernel: the SHA-256 kernels issue VALU work (their HBM traffic is a small fraction
+# of 8 TB/s), the Reed-Solomon encoders stream HBM (read + write) with the GF arithmetic beside it.
+KERNEL_KIND = {"leaf_hash": "valu", "nmt_levels_1": "valu", "nmt_levels": "valu", "dah": "latency",
+               "rs_encode8_rows": "hbm", "rs_encode8_cols": "hbm", "rs_encode16_rows": "hbm", "rs_encode16_cols": "hbm"}
+# SHA-256 compressions per launch of the hashing kernels (B blocks of width k): leaf = 9 per EDS cell, levels 1-2 =
+# 3 per node of the first two levels of all 4k trees, levels 3.. = 3 per remaining inner node
+def kernel_compressions(name, k, B):
+    w = 2 * k
+    if name == "leaf_hash":
+        return 9 * B * w * w
+    if name == "nmt_levels_1":
+        return 3 * B * 2 * w * (w // 2 + w // 4)
+    return None
+
+
+SHA_UBENCH_GCOMP_S = 28.7  # register-only SHA-256 on MI355X (profiles/r02_sha_ubench.txt): the issue-bound ceiling
+VALU_CLK = 2.4e9  # peak engine clock (MI355X_MICROARCH.md)
+
+
+def hbm_ceilings(device):
+    """Measured HBM ceilings of this box (tools/copy_bw.hip, hand-written dwordx4 streaming kernels over 1 GiB
+    buffers): copy (read + write, the RS encoders' traffic shape), read-only, write-only, in GB/s of bytes moved."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libcopybw.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.copybw_measure.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    out = (ctypes.c_double * 3)()
+    cfg = (ctypes.c_int * 3)()
+    if L.copybw_measure(device, 1 << 30, 10, out, cfg) != 0:
+        return None
+    names = ("copy", "read", "write")
+    return {**{f"{n}_gbs": round(out[i], 1) for i, n in enumerate(names)},
+            "best_config": {n: {"accesses_per_thread": cfg[i] // 10000, "workgroup": cfg[i] % 10000}
+                            for i, n in enumerate(names)},
+            "note": "tools/copy_bw.hip: 16 B per lane per access (global_load/store_dwordx4), 1 GiB buffers (4x the "
+                    "Infinity Cache), best of U in {1,2,4,8} x workgroup {256,512,1024}; copy counts read + written "
+                    "bytes"}
+
+
+def isa_mix():
+    """Static VALU mix of the kernels (scripts/isa_mix.sh -> profiles/r*_isa_mix.json, newest)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_isa_mix.json")))
+    if not files:
+        return {}, None
+    mix = json.load(open(files[-1]))
+    return mix, os.path.relpath(files[-1], ROOT)
+
+
+def avg_cycles_per_valu(mix, kernel_symbol_part):
+    for name, v in mix.items():
+        if kernel_symbol_part in name:
+            return v["avg_cycles_per_valu"]
     return None
 
 
@@ -133,14 +179,33 @@ def _host_topology():
     return {"nproc": os.cpu_count(), "affinity": aff, "physical_cores": len(phys) or None, "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(k, seconds):
-    """The CPU restatement (oracle/, 'port') on this host's cores: whole single-threaded
-    ExtendShares+NewDataAvailabilityHeader calls on independent blocks, one worker per thread,
-    swept over 1 / 16 / 64 / all threads of the affinity mask (all = `cores`)."""
+def _best_ms(fn, reps):
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        el = (time.perf_counter() - t0) * 1e3
+        best = el if best is None else min(best, el)
+    return best
+
+
+def cpu_baseline(k, seconds, gpu=None):
+    """The CPU restatement (oracle/, 'port': the Go reference cannot run here) on this host's cores, in the shapes
+    SURVEY.md §8d prescribes, each next to its GPU number (`gpu`: the GPU extras of this run):
+    * throughput (`value`): whole single-threaded ExtendShares+NewDataAvailabilityHeader calls on independent k=128
+      blocks, one per worker thread, swept over 1 / 16 / 64 / all threads of the affinity mask;
+    * single_block_ms: ONE k=128 block (the consensus path handles one block at a time,
+      app/process_proposal.go:137,143) with rsmt2d's axis fan-out -- one task per row / column in every phase
+      (oracle/da.c parallel_for) -- on 1, 16, the cgroup quota and all threads;
+    * repair_c4_ms: config C4 (k=128 Repair, random 50 % and Q0-only) single-threaded like rsmt2d's solveCrossword,
+      with klauspost's Leopard reconstruct as the decoder (ora_leo_decode_fft);
+    * k512_ms: config C5 (one k=512 square, GF(2^16)) with axis fan-out;
+    * blob_commitments: go-square CreateCommitment of 64 KiB blobs on one thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     topo = _host_topology()
     allt = topo["affinity"]
+    quota = int(topo["cgroup_cpu_quota"]) if topo["cgroup_cpu_quota"] else allt
     ods = gen_ods(k, 0xC0FFEE)
     counts = sorted({1, min(16, allt), min(64, allt), allt})
     sweep, total_blocks = {}, {}
@@ -151,19 +216,60 @@ def cpu_baseline(k, seconds):
     model, flags = _host_cpu()
     best = max(sweep, key=lambda n: sweep[n])
     phys = topo["physical_cores"] or allt
-    return {"value": sweep[best], "unit": "blocks/s", "cores": int(best), "kind": "port",
-            "single_thread_value": sweep["1"], "sweep_threads_blocks_per_s": sweep,
-            "all_threads": {"threads": allt, "value": sweep[str(allt)]},
-            "full_host_linear_extrapolation": {"cores": phys, "value": round(sweep["1"] * phys, 1),
-                                               "note": "single-thread rate x physical cores: an upper bound for "
-                                                       "the whole host, not a measurement (the bench process is "
-                                                       "limited by its cgroup CPU quota)"},
-            "host": dict(topo, cpu=model, simd=flags),
-            "sample": f"k={k} ExtendShares+NewDataAvailabilityHeader (EDS written) via oracle/liboracle.so "
-                      f"(C restatement, OpenSSL SHA-256 (SHA-NI), AVX2 Leopard; not the Go reference): independent "
-                      f"blocks, one single-threaded call per worker thread, {seconds / len(counts):.1f} s per thread "
-                      f"count over 1..{allt} threads of the affinity mask; value = the best count (the cgroup CPU "
-                      f"quota is {topo['cgroup_cpu_quota']} CPUs); (blocks, s) per count: {total_blocks}"}
+    out = {"value": sweep[best], "unit": "blocks/s", "cores": int(best), "kind": "port",
+           "single_thread_value": sweep["1"], "sweep_threads_blocks_per_s": sweep,
+           "all_threads": {"threads": allt, "value": sweep[str(allt)]},
+           "full_host_linear_extrapolation": {"cores": phys, "value": round(sweep["1"] * phys, 1),
+                                              "note": "single-thread rate x physical cores: an upper bound for "
+                                                      "the whole host, not a measurement (the bench process is "
+                                                      "limited by its cgroup CPU quota)"},
+           "host": dict(topo, cpu=model, simd=flags)}
+    # one block, axis fan-out (EDS written: da.ExtendShares returns it)
+    lat_threads = sorted({1, min(16, allt), min(quota, allt), allt})
+    out["single_block_ms"] = {str(n): round(_best_ms(lambda: O.extend_commit(ods, nthreads=n), 3 if n > 1 else 2), 2)
+                              for n in lat_threads}
+    # config C4 on the CPU
+    w = 2 * k
+    rc, eds, rr, cr, _ = O.extend_commit(ods, nthreads=min(quota, allt))
+    rng = np.random.default_rng(7)
+    q0 = np.zeros((w, w), np.uint8)
+    q0[:k, :k] = 1
+    c4 = {}
+    for name, pres in (("random", (rng.random(w * w) < 0.5).astype(np.uint8)), ("q0_only", q0.reshape(-1))):
+        damaged = eds.copy()
+        damaged[pres == 0] = 0
+        res = {}
+        c4[name] = round(_best_ms(lambda: res.setdefault("r", O.repair(damaged, pres, rr, cr, fft=True)), 2), 1)
+        if res["r"][0] != 0 or not np.array_equal(res["r"][1], eds):
+            raise RuntimeError(f"CPU repair ({name}) did not restore the square")
+    out["repair_c4_ms"] = dict(c4, note="k=128, single thread (rsmt2d's crossword is sequential), decoder = "
+                                        "Leopard reconstruct (ora_leo_decode_fft); same damaged squares as repair_c4")
+    # config C5 on the CPU
+    ods512 = gen_ods(512, 0xC0FFEE)
+    nq = min(quota, allt)
+    k5 = {}
+    r5 = {}
+    k5[str(nq)] = round(_best_ms(lambda: r5.setdefault("r", O.extend_commit(ods512, want_eds=True, nthreads=nq)), 2), 1)
+    k5["1"] = round(_best_ms(lambda: O.extend_commit(ods512, want_eds=False, nthreads=1), 1), 1)
+    out["k512_ms"] = dict(k5, note="one k=512 square (GF(2^16)), EDS written, axis fan-out; keys = threads")
+    out["k512_dah"] = r5["r"][4].hex()
+    # blob share commitments on one thread, the bench's blobs; equal to the GPU's when this run computed them
+    ns, data, offs = commitment_blobs()
+    size = int(offs[1])
+    n_cpu, t0 = 0, time.perf_counter()
+    while n_cpu < len(offs) - 1 and time.perf_counter() - t0 < 2.0:
+        rc, c = O.blob_commitment(ns[29 * n_cpu:29 * n_cpu + 29].tobytes(), data[n_cpu * size:(n_cpu + 1) * size].tobytes())
+        if rc != 0 or (gpu and gpu.get("commitments") is not None and c != gpu["commitments"][n_cpu].tobytes()):
+            raise RuntimeError("GPU blob commitment differs from the CPU restatement's")
+        n_cpu += 1
+    out["blob_commitments_1thread_per_s"] = round(n_cpu / (time.perf_counter() - t0), 1)
+    out["sample"] = (f"k={k} ExtendShares+NewDataAvailabilityHeader (EDS written) via oracle/liboracle.so (C "
+                     f"restatement, OpenSSL SHA-256 (SHA-NI), AVX2 Leopard; not the Go reference): throughput = "
+                     f"independent blocks, one single-threaded call per worker thread, {seconds / len(counts):.1f} s "
+                     f"per thread count over 1..{allt} threads (cgroup quota {topo['cgroup_cpu_quota']} CPUs), "
+                     f"(blocks, s) per count: {total_blocks}; single_block_ms / repair_c4_ms / k512_ms: best of 1-3 "
+                     f"calls; blob commitments: 64 KiB blobs")
+    return out
 
 
 def repair_measure(ctx, k=128, survive=0.5, reps=5, warmup=2):
@@ -222,10 +328,9 @@ def repair_measure(ctx, k=128, survive=0.5, reps=5, warmup=2):
 
 
 # bench kernel name -> rocprofv3 kernel name in profiles/*_counters.json
-PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "nmt_level1": "nmt_level_kernel<true>", "dah": "dah_kernel",
-             "nmt_levels_1": "nmt_levels_kernel", "nmt_levels": "nmt_levels_kernel",
-             "rs_rows_leaf": "rs_rows_leaf_kernel<7>", "rs_cols_leaf": "rs_cols_leaf_kernel<7>",
-             "rs_encode8_rows": "rs_encode8_g2_kernel<7>", "rs_encode8_cols": "rs_encode8_g2_kernel<7>"}
+# (only kernels with ONE dispatch per step: the summaries average the counters over all dispatches of a kernel name,
+# so the RS rows / columns launches and the tree-level launches would be mixed)
+PMC_NAMES = {"leaf_hash": "leaf_hash_kernel", "dah": "dah_kernel"}
 PMC_BATCH = 128  # scripts/profile.sh profiles the default bench step (B = 128 blocks)
 
 
@@ -251,13 +356,8 @@ def pmc_counters(kernel, B):
         if not c:
             continue
         scale = B / float(c.get("bench_batch", PMC_BATCH))
-        busy = None
-        if c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
-            # SQ_ACTIVE_INST_VALU: quad-cycles of VALU issue summed over the 1024 SIMDs; GRBM_GUI_ACTIVE: cycles x 8 XCDs
-            busy = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * c["GRBM_GUI_ACTIVE"] / 8)
         return {"hbm_bytes": int(c["hbm_bytes_corrected"] * scale) if "hbm_bytes_corrected" in c else None,
                 "valu_insts": c["SQ_INSTS_VALU"] * scale if "SQ_INSTS_VALU" in c else None,
-                "valu_busy": busy,
                 "source": f"{os.path.relpath(f, ROOT)} ({PMC_NAMES[kernel]}, B={c.get('bench_batch', PMC_BATCH)} "
                           f"profile scaled to B={B})"}
     return None
@@ -332,7 +432,12 @@ def k512_measure(ctx, dev, reps=3):
     torch.cuda.synchronize(dev)
     prof = ctx.profile_read()
     ctx.profile_enable(False)
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")))["k512"]
+    for b in range(B):
+        if bytes(dah[b].cpu().numpy()).hex() != want[str(0xC0FFEE + b)]:
+            raise RuntimeError(f"k=512 block {b} DAH differs from the committed digest")
     out = {"k": k, "blocks_per_call": B, "ms_per_block": round(el * 1e3 / B, 3), "blocks_per_s": round(B / el, 2),
+           "dah_golden": want[str(0xC0FFEE)], "dahs_checked_vs_golden": B,
            "path_hbm_gbs": round(block_bytes(k) * B / el / 1e9, 1),
            "kernels_ms": {n: round(ms / max(1, cnt), 3) for n, (ms, cnt) in prof.items()},
            "parity": "GF(2^16) unpinned by reference data (Lagrange-oracle checked)"}
@@ -442,15 +547,21 @@ def host_path_measure(ctx, k, nblocks=48, reps=3):
     return out
 
 
-def commitments_measure(ctx, nblobs=256, size=64 * 1024, reps=5):
-    """x/blob share commitments (inclusion.CreateCommitments) of a batch of random blobs: one cda_blob_commitments
-    call on pre-packed host arrays (H2D of the blob data included), next to the C oracle on one host thread."""
+def commitment_blobs(nblobs=256, size=64 * 1024):
+    """The bench's blob batch: random 64 KiB blobs under random v0 namespaces (seeded)."""
     rng = np.random.default_rng(11)
     data = rng.integers(0, 256, nblobs * size, dtype=np.uint8)
     ns = np.zeros((nblobs, 29), np.uint8)
     ns[:, 19:] = rng.integers(0, 256, (nblobs, 10), dtype=np.uint8)
-    ns = ns.reshape(-1)
-    offs = np.arange(nblobs + 1, dtype=np.uint64) * size
+    return ns.reshape(-1), data, np.arange(nblobs + 1, dtype=np.uint64) * size
+
+
+def commitments_measure(ctx, reps=5):
+    """x/blob share commitments (inclusion.CreateCommitments) of a batch of random blobs: one cda_blob_commitments
+    call on pre-packed host arrays (H2D of the blob data included).  The CPU leg (cpu_baseline) recomputes the
+    first ones with the oracle and compares."""
+    ns, data, offs = commitment_blobs()
+    nblobs, size = len(offs) - 1, int(offs[1])
     got = ctx.blob_commitments_packed(ns, data, offs)
     best = None
     for _ in range(reps):
@@ -458,19 +569,9 @@ def commitments_measure(ctx, nblobs=256, size=64 * 1024, reps=5):
         ctx.blob_commitments_packed(ns, data, offs)
         el = time.perf_counter() - t0
         best = el if best is None else min(best, el)
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
-    n_cpu, t0 = 0, time.perf_counter()
-    while n_cpu < nblobs and time.perf_counter() - t0 < 2.0:
-        rc, c = O.blob_commitment(ns[29 * n_cpu:29 * n_cpu + 29].tobytes(), data[n_cpu * size:(n_cpu + 1) * size].tobytes())
-        if rc != 0 or c != got[n_cpu].tobytes():
-            raise RuntimeError("blob commitment differs from the oracle")
-        n_cpu += 1
-    cpu = n_cpu / (time.perf_counter() - t0)
     return {"blobs": nblobs, "blob_bytes": size, "ms": round(best * 1e3, 3), "blobs_per_s": round(nblobs / best, 1),
-            "mb_per_s": round(nblobs * size / best / 1e6, 1), "cpu_port_1thread_blobs_per_s": round(cpu, 1),
-            "note": "one cda_blob_commitments call incl. H2D of the blob data (pageable), threshold 64; CPU: "
-                    "oracle/inclusion.c on 1 thread (OpenSSL SHA-256), first results checked bit-exact"}
+            "mb_per_s": round(nblobs * size / best / 1e6, 1),
+            "note": "one cda_blob_commitments call incl. H2D of the blob data (pageable), threshold 64"}, got
 
 
 def launch_ranks(args):
@@ -581,10 +682,12 @@ def main():
     ctx = cda.Context(dev.index)
     k, B = args.k, args.batch
     w = 2 * k
-    # synthetic, distinct blocks per rank (seed = 0xC0FFEE + global block index)
-    base = [gen_ods(k, 0xC0FFEE + rank * B + b) for b in range(min(B, 4))]
-    ods_host = np.stack([base[b % len(base)] for b in range(B)])
+    # synthetic blocks, DISTINCT different squares per rank (seed = 0xC0FFEE + rank * B + b), replicated to fill B
+    nd = min(B, DISTINCT_ODS)
+    base = [gen_ods(k, 0xC0FFEE + rank * B + b) for b in range(nd)]
+    ods_host = np.stack([base[b % nd] for b in range(B)])
     d_ods = torch.from_numpy(ods_host).to(dev)
+    del ods_host
     d_eds = torch.empty((B, w * w, 512), dtype=torch.uint8, device=dev)
     d_roots = torch.empty((B, 2 * w, 96), dtype=torch.uint8, device=dev)
     d_dah = torch.empty((B, 32), dtype=torch.uint8, device=dev)
@@ -615,6 +718,8 @@ def main():
     blocks = world * B * args.steps
     value = blocks / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
+    # the timed steps' output: every block's DAH against the committed digests (tests/golden/bench_digests.json)
+    check = check_dahs(d_dah.cpu().numpy(), k, B, rank, nd)
 
     # per-kernel durations: HIP events on the launch stream, separate pass (profiling adds event records)
     ctx.profile_reset()
@@ -626,40 +731,14 @@ def main():
     prof = ctx.profile_read()
     ctx.profile_enable(False)
     kern = {n: {"avg_ms": ms / max(1, cnt), "launches": cnt, "total_ms": ms} for n, (ms, cnt) in prof.items()}
-    dom = max(kern, key=lambda n: kern[n]["total_ms"])
-    HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    clk = 2.4e9  # max engine clock, MI355X_MICROARCH.md
-    # VALU issue peak: every SIMD (4 per CU) issues one wave64 instruction per 2 cycles
-    valu_peak_tops = ncu * 4 * clk / VALU_CYCLES_PER_WAVE_INSTR * 64 / 1e12
-    dom_step_bytes = kernel_step_bytes(dom, k, B)
-    launches_per_step = max(1, kern[dom]["launches"] // prof_steps)
-    dom_launch_bytes = dom_step_bytes // launches_per_step if dom_step_bytes else None
-    dom_avg_s = kern[dom]["avg_ms"] * 1e-3
-    hbm_gbs = dom_launch_bytes / dom_avg_s / 1e9 if dom_launch_bytes else None
-    pmc = pmc_counters(dom, B)
+    ceil = hbm_ceilings(dev.index) if rank == 0 else None
+    mix, mix_src = isa_mix()
+    rooflines = {n: kernel_roofline(n, kern[n], k, B, prof_steps, ncu, ceil, mix) for n in kern}
+    dom = max(kern, key=lambda n: kern[n]["total_ms"])
+    roofline = dict(rooflines[dom], kernel=dom)
     path_gbs = block_bytes(k) * value / world / 1e9
     comp_per_s = block_compressions_engine(k) * value / world
-
-    roofline = {"kernel": dom, "avg_launch_ms": round(kern[dom]["avg_ms"], 4), "bytes_per_launch": dom_launch_bytes,
-                "traffic": pmc["hbm_bytes"] if pmc else None}
-    if pmc and pmc.get("valu_insts"):
-        achieved = pmc["valu_insts"] * 64 / dom_avg_s / 1e12
-        roofline.update({"bound": "valu", "achieved": round(achieved, 2), "peak": round(valu_peak_tops, 2),
-                         "unit": "TOPS", "frac": round(achieved / valu_peak_tops, 4),
-                         "valu_wave_instr_per_launch": int(pmc["valu_insts"]),
-                         "peak_def": f"{ncu} CU x 4 SIMD x 2.4 GHz / 2 cycles per wave64 VALU instruction x 64 lanes "
-                                     "(int32 lane-ops/s)",
-                         "hbm": {"achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK, "unit": "GB/s",
-                                 "frac": round(hbm_gbs / HBM_PEAK, 4) if hbm_gbs else None},
-                         "valu_busy_pmc": round(pmc["valu_busy"], 3) if pmc.get("valu_busy") else None,
-                         "valu_busy_def": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x kernel cycles): fraction of the "
-                                          "kernel's cycles the VALU was issuing; frac < busy because 57 % of SHA-256's "
-                                          "instructions take 4 cycles, not 2 (DESIGN.md §4)",
-                         "counters_source": pmc["source"]})
-    else:  # no PMC pass covers this kernel: HBM view only
-        roofline.update({"bound": "hbm", "achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK,
-                         "unit": "GB/s", "frac": round(hbm_gbs / HBM_PEAK, 4) if hbm_gbs else None})
 
     result = {
         "metric": "ODS->EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s",
@@ -673,35 +752,140 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (namespace-sorted random shares, SplitMix64 seed 0xC0FFEE+block)",
+        "data": f"synthetic (namespace-sorted random shares, SplitMix64 seed 0xC0FFEE+rank*B+b, {nd} distinct "
+                f"squares per rank replicated to B)",
         "config": {"workload": f"k{k}_block_batch: da.ExtendShares+NewDataAvailabilityHeader on {B} independent "
                                f"k={k} blocks per GPU per step (configs[1] per block, batched as configs[2])",
                    "k": k, "blocks_per_gpu_per_step": B, "share_size": 512,
                    "parallelism": f"blocks x{world}" + (" (ranks share one device, gloo)" if shared else "")},
         "roofline": roofline,
+        "kernel_rooflines": {n: v for n, v in rooflines.items() if n != dom},
+        "hbm_ceilings": ceil,
+        "isa_mix_source": mix_src,
+        "output_check": check,
         "path_hbm_gbs": round(path_gbs, 1),
         "sha256_compressions_per_s": comp_per_s,
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
+    gpu = {}
     if rank == 0 and world == 1 and not args.no_extras:
+        del d_eds, d_roots, d_ods
+        torch.cuda.empty_cache()
         result["c2_single_block"] = single_block_measure(ctx, dev)
         result["repair_c4"] = repair_measure(ctx)
-        result["blob_commitments"] = commitments_measure(ctx)
+        result["blob_commitments"], gpu["commitments"] = commitments_measure(ctx)
         result["host_buffers"] = host_path_measure(ctx, k)
         result["share_proof"] = proof_measure(ctx, k)
         result["k512_single"] = k512_measure(ctx, dev)
         result["device_square"] = square_measure(ctx)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(k, args.cpu_seconds)
-        cb = result["cpu_baseline"]
-        result["gpu_vs_cpu"] = {"measured_best": round(value / cb["value"], 1),
-                                "full_host_linear_extrapolation": round(
-                                    value / cb["full_host_linear_extrapolation"]["value"], 1)}
+        result["cpu_baseline"] = cb = cpu_baseline(k, args.cpu_seconds, gpu)
+        result["gpu_vs_cpu"] = gpu_vs_cpu(result, value)
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+DISTINCT_ODS = 16  # distinct synthetic squares per rank (tests/golden/make_bench_digests.py covers ranks 0..7)
+
+
+def check_dahs(dah, k, B, rank, nd):
+    """Every block's DAH of the timed steps against tests/golden/bench_digests.json (oracle DAHs of the bench's
+    seeds); replicas of one square must agree too."""
+    path = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+    want = json.load(open(path)).get(f"k{k}", {}) if os.path.exists(path) else {}
+    checked = 0
+    for b in range(B):
+        got = bytes(dah[b]).hex()
+        if got != bytes(dah[b % nd]).hex():
+            raise RuntimeError(f"block {b} DAH differs from its replica {b % nd}")
+        exp = want.get(str(0xC0FFEE + rank * B + b % nd))
+        if exp is not None:
+            if got != exp:
+                raise RuntimeError(f"block {b} DAH {got} != committed digest {exp}")
+            checked += 1
+    return {"blocks_checked_vs_golden": checked, "distinct_squares": nd, "source": "tests/golden/bench_digests.json"}
+
+
+def kernel_roofline(name, kv, k, B, prof_steps, ncu, ceil, mix):
+    """Roofline of one kernel of the bench step, by what bounds it (KERNEL_KIND): HBM kernels against 8 TB/s and the
+    measured copy ceiling; VALU kernels against the wave64 issue peak, cycle-weighted by their static instruction mix
+    (tools/isa_count.py) and, for the SHA-256 kernels, against the register-only SHA-256 ceiling."""
+    HBM_PEAK = 8000.0  # GB/s, MI355X_MICROARCH.md
+    kind = KERNEL_KIND.get(name, "hbm")
+    launches_per_step = max(1, kv["launches"] // prof_steps)
+    avg_s = kv["avg_ms"] * 1e-3
+    step_bytes = kernel_step_bytes(name, k, B)
+    launch_bytes = step_bytes // launches_per_step if step_bytes else None
+    gbs = launch_bytes / avg_s / 1e9 if launch_bytes else None
+    pmc = pmc_counters(name, B)
+    r = {"bound": "valu" if kind in ("valu", "latency") else "hbm", "avg_launch_ms": round(kv["avg_ms"], 4),
+         "bytes_per_launch": launch_bytes, "traffic": pmc["hbm_bytes"] if pmc else None}
+    hbm = {"achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK, 4) if gbs else None}
+    if ceil and gbs:
+        hbm["measured_copy_ceiling"] = ceil["copy_gbs"]
+        hbm["frac_of_measured_copy"] = round(gbs / ceil["copy_gbs"], 4)
+    if r["bound"] == "hbm":
+        r.update(achieved=hbm["achieved"], peak=HBM_PEAK, unit="GB/s", frac=hbm["frac"])
+        if "frac_of_measured_copy" in hbm:
+            r["frac_of_measured_copy"] = hbm["frac_of_measured_copy"]
+            r["measured_copy_ceiling_gbs"] = hbm["measured_copy_ceiling"]
+        return r
+    r["hbm"] = hbm
+    peak = ncu * 4 * VALU_CLK / VALU_CYCLES_PER_WAVE_INSTR * 64 / 1e12
+    if pmc and pmc.get("valu_insts"):
+        achieved = pmc["valu_insts"] * 64 / avg_s / 1e12
+        r.update(achieved=round(achieved, 2), peak=round(peak, 2), unit="TOPS", frac=round(achieved / peak, 4),
+                 valu_wave_instr_per_launch=int(pmc["valu_insts"]), counters_source=pmc["source"],
+                 peak_def=f"{ncu} CU x 4 SIMD x 2.4 GHz / 2 cycles per wave64 VALU instruction x 64 lanes")
+        sym = {"leaf_hash": "leaf_hash_kernel", "nmt_levels_1": "nmt_levels_kernel", "nmt_levels": "nmt_levels_kernel",
+               "dah": "dah_kernel"}.get(name)
+        cyc = avg_cycles_per_valu(mix, sym) if sym else None
+        if cyc:
+            # issue cycles the kernel's instructions occupy, priced with the measured per-instruction costs (2 or 4
+            # cycles, DESIGN.md §4) at the static mix's average, over the SIMD-cycles of the launch at 2.4 GHz
+            r["valu_cycle_weighted"] = {
+                "avg_cycles_per_instr": cyc,
+                "busy": round(pmc["valu_insts"] * cyc / (ncu * 4 * VALU_CLK * avg_s), 4),
+                "def": "SQ_INSTS_VALU x static-mix cycles per instruction / (SIMDs x 2.4 GHz x launch time)"}
+    comp = kernel_compressions(name, k, B)
+    if comp:
+        g = comp / launches_per_step / avg_s / 1e9 if name != "leaf_hash" else comp / avg_s / 1e9
+        r["sha256"] = {"achieved_gcomp_s": round(g, 2), "ceiling_gcomp_s": SHA_UBENCH_GCOMP_S,
+                       "frac": round(g / SHA_UBENCH_GCOMP_S, 4),
+                       "ceiling_def": "register-only SHA-256 microbenchmark (profiles/r02_sha_ubench.txt)"}
+    return r
+
+
+def gpu_vs_cpu(result, value):
+    cb = result["cpu_baseline"]
+    out = {"throughput_measured_best": round(value / cb["value"], 1),
+           "throughput_full_host_linear_extrapolation": round(value / cb["full_host_linear_extrapolation"]["value"], 1)}
+    lat = cb.get("single_block_ms", {})
+    if lat:
+        best_cpu = min(lat.values())
+        out["single_block_cpu_best_ms"] = best_cpu
+        if "c2_single_block" in result:
+            out["single_block_device_resident"] = round(best_cpu / result["c2_single_block"]["ms"], 1)
+        hb = result.get("host_buffers", {}).get("one_block_latency_ms", {})
+        if hb.get("with_eds"):
+            out["single_block_host_buffers_with_eds"] = round(best_cpu / hb["with_eds"], 1)
+    c4 = cb.get("repair_c4_ms", {})
+    g4 = result.get("repair_c4", {})
+    for case in ("random", "q0_only"):
+        if case in c4 and case in g4:
+            out[f"repair_{case}_host_buffers"] = round(c4[case] / g4[case]["ms_median"], 1)
+            out[f"repair_{case}_device_resident"] = round(c4[case] / g4[case]["device_resident_ms_median"], 1)
+    k5 = cb.get("k512_ms", {})
+    g5 = result.get("k512_single", {})
+    if k5 and g5:
+        out["k512_block_path"] = round(min(v for kk, v in k5.items() if kk != "note") / g5["ms_per_block"], 1)
+        if g5.get("dah_golden") and cb.get("k512_dah") != g5["dah_golden"]:
+            raise RuntimeError("CPU k=512 DAH differs from the committed digest")
+    return out
 
 
 def bench_split(args):

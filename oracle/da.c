@@ -414,6 +414,7 @@ typedef struct {
   uint8_t* present;
   const uint8_t* row_roots;
   const uint8_t* col_roots;
+  int fft_decoder; /* 1: klauspost's Leopard reconstruct, 0: Lagrange (independent check) */
 } rep_t;
 
 static uint8_t* rcell(rep_t* R, int axis, int idx, int i) {
@@ -484,7 +485,7 @@ static int solve_axis(rep_t* R, int axis, int idx, int* solved, int* progress, i
     pres[i] = (uint8_t)rpresent(R, axis, idx, i);
     if (pres[i]) memcpy(sh[i], rcell(R, axis, idx, i), R->L);
   }
-  int rc = ora_leo_decode(k, R->L, sh, pres);
+  int rc = R->fft_decoder ? ora_leo_decode_fft(k, R->L, sh, pres) : ora_leo_decode(k, R->L, sh, pres);
   if (rc != ORA_OK) { /* not decodable yet: no progress, no error */
     free(buf);
     free(sh);
@@ -531,7 +532,12 @@ out:
 
 int ora_repair(int k, size_t share_len, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, int* err_axis, int* err_index) {
-  rep_t R = {k, 2 * k, share_len, eds, present, row_roots, col_roots};
+  return ora_repair_ex(k, share_len, eds, present, row_roots, col_roots, err_axis, err_index, 0);
+}
+
+int ora_repair_ex(int k, size_t share_len, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+                  const uint8_t* col_roots, int* err_axis, int* err_index, int fft_decoder) {
+  rep_t R = {k, 2 * k, share_len, eds, present, row_roots, col_roots, fft_decoder};
   int w = 2 * k;
   /* prerepairSanityCheck */
   for (int i = 0; i < w; i++) {

@@ -13,10 +13,14 @@
  * over the data placed at points m..m+k-1 followed by FFT-DIT to points
  * 0..k-1 ("mtrunc" loop bounds, multiplier log == modulus => XOR only).
  *
- * Decode is deliberately NOT the Leopard error-locator path: it is Lagrange
- * interpolation in Leopard's field, an independent decoder.  Because the code
- * is MDS every correct decoder returns identical bytes, so agreement between
- * this decoder and the FFT encoder pins the closed form used on the GPU.
+ * ora_leo_decode is deliberately NOT the Leopard error-locator path: it is
+ * Lagrange interpolation in Leopard's field, an independent decoder.  Because
+ * the code is MDS every correct decoder returns identical bytes, so agreement
+ * between this decoder and the FFT encoder pins the closed form used on the GPU.
+ * ora_leo_decode_fft restates klauspost's own reconstruct (error locators,
+ * IFFT, formal derivative, FFT: O(k log k) per shard byte) -- the CPU baseline
+ * of the repair path (bench.py cpu_baseline.repair_c4), checked against the
+ * Lagrange decoder in tests/test_oracle.py.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -373,5 +377,94 @@ int ora_leo_decode(int k, size_t shard_len, uint8_t* const* shards, const uint8_
   free(xs);
   free(src);
   free(w);
+  return ORA_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Leopard reconstruct (klauspost/reedsolomon v1.12.1 leopardFF8/FF16  */
+/* reconstruct, upstream; restated for the CPU baseline)               */
+/* ------------------------------------------------------------------ */
+
+/* ifftDITDecoder: as the encoder's IFFT but with skew[iend - 1] and an mtrunc bound */
+static void ifft_dit_decoder(const field_t* f, uint8_t** work, int mtrunc, int m, const uint16_t* skew, size_t n) {
+  int dist = 1, dist4 = 4;
+  while (dist4 <= m) {
+    for (int r = 0; r < mtrunc; r += dist4) {
+      int iend = r + dist;
+      unsigned l01 = skew[iend - 1], l02 = skew[iend + dist - 1], l23 = skew[iend + 2 * dist - 1];
+      for (int i = r; i < iend; i++) {
+        ifft2(f, work[i], work[i + dist], l01, n);
+        ifft2(f, work[i + 2 * dist], work[i + 3 * dist], l23, n);
+        ifft2(f, work[i], work[i + 2 * dist], l02, n);
+        ifft2(f, work[i + dist], work[i + 3 * dist], l02, n);
+      }
+    }
+    dist = dist4;
+    dist4 <<= 2;
+  }
+  if (dist < m) {
+    unsigned logm = skew[dist - 1];
+    for (int i = 0; i < dist; i++) ifft2(f, work[i], work[i + dist], logm, n);
+  }
+}
+
+/* FormalDerivative: for i = 1..n-1, width = ((i ^ (i-1)) + 1) / 2, work[i-width..i) ^= work[i..i+width) */
+static void formal_derivative(uint8_t** work, int nn, size_t n) {
+  for (int i = 1; i < nn; i++) {
+    int width = ((i ^ (i - 1)) + 1) >> 1;
+    for (int j = 0; j < width; j++) slice_xor(work[i - width + j], work[i + j], n);
+  }
+}
+
+int ora_leo_decode_fft(int k, size_t shard_len, uint8_t* const* shards, const uint8_t* present) {
+  if (k <= 0 || k > 32768) return ORA_E_ARG;
+  if (shard_len == 0 || shard_len % 64 != 0) return ORA_E_SHARD_SIZE;
+  const field_t* f = field_for_bits(ora_leo_bits_for(k));
+  const int m = ceil_pow2(k), nn = 2 * m;
+  int npresent = 0;
+  for (int s = 0; s < 2 * k; s++) npresent += present[s] ? 1 : 0;
+  if (npresent < k) return ORA_E_TOO_FEW;
+  if (npresent == 2 * k) return ORA_OK;
+  /* erasures in the n-space: parity i -> i, the padding [k, m), data i -> m + i */
+  uint8_t* erased = (uint8_t*)calloc((size_t)nn, 1);
+  for (int i = 0; i < k; i++)
+    if (!present[k + i]) erased[i] = 1;
+  for (int i = k; i < m; i++) erased[i] = 1;
+  for (int i = 0; i < k; i++)
+    if (!present[i]) erased[m + i] = 1;
+  /* error locators: errLocs[p] = sum_{j erased} log(p ^ j) mod modulus, log(0) := 0 (the value klauspost's two
+   * Walsh-Hadamard transforms produce) */
+  unsigned* loc = (unsigned*)malloc(sizeof(unsigned) * (size_t)nn);
+  for (int p = 0; p < nn; p++) {
+    unsigned long long acc = 0;
+    for (int j = 0; j < nn; j++)
+      if (erased[j] && j != p) acc += f->log_t[p ^ j];
+    loc[p] = (unsigned)(acc % f->modulus);
+  }
+  uint8_t* buf = (uint8_t*)aligned_alloc(64, (size_t)nn * shard_len);
+  uint8_t** work = (uint8_t**)malloc(sizeof(uint8_t*) * (size_t)nn);
+  memset(buf, 0, (size_t)nn * shard_len);
+  for (int i = 0; i < nn; i++) work[i] = buf + (size_t)i * shard_len;
+  for (int i = 0; i < k; i++) {
+    if (present[k + i]) mul_add(f, work[i], shards[k + i], loc[i], shard_len);
+    if (present[i]) mul_add(f, work[m + i], shards[i], loc[m + i], shard_len);
+  }
+  ifft_dit_decoder(f, work, m + k, nn, f->skew, shard_len);
+  formal_derivative(work, nn, shard_len);
+  fft_dit(f, work, m + k, nn, f->skew, shard_len);
+  for (int i = 0; i < k; i++) {
+    if (!present[i]) {
+      memset(shards[i], 0, shard_len);
+      mul_add(f, shards[i], work[m + i], (f->modulus - loc[m + i]) % f->modulus, shard_len);
+    }
+    if (!present[k + i]) {
+      memset(shards[k + i], 0, shard_len);
+      mul_add(f, shards[k + i], work[i], (f->modulus - loc[i]) % f->modulus, shard_len);
+    }
+  }
+  free(work);
+  free(buf);
+  free(loc);
+  free(erased);
   return ORA_OK;
 }

@@ -69,6 +69,9 @@ int ora_leo_encode(int k, size_t shard_len, const uint8_t* const* data, uint8_t*
  * Uses Lagrange interpolation over Leopard's field, a decoder independent from
  * the FFT path (MDS => any correct decoder returns identical bytes). */
 int ora_leo_decode(int k, size_t shard_len, uint8_t* const* shards, const uint8_t* present);
+/* The same erasure decode through klauspost's own Leopard reconstruct (error locators, IFFT, formal derivative,
+ * FFT): O(k log k) per shard byte, the CPU baseline's decoder (bench.py).  Checked against ora_leo_decode. */
+int ora_leo_decode_fft(int k, size_t shard_len, uint8_t* const* shards, const uint8_t* present);
 /* Field helpers (Leopard representation) exposed for property tests. */
 unsigned ora_leo_mul(int bits, unsigned a, unsigned b);
 int ora_leo_skew(int bits, int i);      /* FFT skew log table entry */
@@ -105,6 +108,9 @@ int ora_extend_commit(int count, size_t share_len, const uint8_t* shares, uint8_
  * Returns ORA_OK, ORA_E_UNREPAIRABLE or ORA_E_BYZANTINE (with axis/index). */
 int ora_repair(int k, size_t share_len, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
                const uint8_t* col_roots, int* err_axis, int* err_index);
+/* ora_repair with the decoder chosen: fft_decoder = 0 Lagrange (ora_repair), 1 Leopard reconstruct. */
+int ora_repair_ex(int k, size_t share_len, uint8_t* eds, uint8_t* present, const uint8_t* row_roots,
+                  const uint8_t* col_roots, int* err_axis, int* err_index, int fft_decoder);
 
 /* ---- NMT building blocks (da.c) ---- */
 void ora_nmt_hash_node_ns(int ns_len, const uint8_t* l, const uint8_t* r, uint8_t* out);

@@ -50,14 +50,15 @@ json.dump(summary, open(os.path.join(dst, f"{tag}_counters.json"), "w"), indent=
 with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
     f.write(f"# rocprofv3 summary ({tag})\n\nSource: scripts/profile.sh (bench.py --steps 5 --warmup 1), "
             "kernel trace + separate PMC passes.\n\n")
-    f.write("| kernel | avg ns | dispatches | VALU instr/wave | issue-stall frac | waitcnt/barrier frac | FETCH KB | WRITE KB | eff. clock GHz | VALU busy (ACTIVE_INST_VALU) |\n|---|---|---|---|---|---|---|---|---|---|\n")
+    f.write("| kernel | avg ns | dispatches | VALU instr/wave | issue-stall frac | waitcnt/barrier frac | FETCH KB | WRITE KB | eff. clock GHz | VALU issue frac (2-cycle) |\n|---|---|---|---|---|---|---|---|---|---|\n")
     for k, r in sorted(summary.items(), key=lambda kv: -kv[1].get("avg_duration_ns", 0) * kv[1].get("dispatches", 0)):
         vpw = r.get("SQ_INSTS_VALU", 0) / r["SQ_WAVES"] if r.get("SQ_WAVES") else 0
         stall = r.get("SQ_WAIT_INST_ANY", 0) / r["SQ_WAVE_CYCLES"] if r.get("SQ_WAVE_CYCLES") else 0
         wait = r.get("SQ_WAIT_ANY", 0) / r["SQ_WAVE_CYCLES"] if r.get("SQ_WAVE_CYCLES") else 0
         clk = r.get("GRBM_GUI_ACTIVE", 0) / 8 / r["avg_duration_ns"] if r.get("avg_duration_ns") else 0
-        # SQ_ACTIVE_INST_VALU: quad-cycles waves spend issuing VALU, summed over the chip's 1024 SIMDs
-        busy = r.get("SQ_ACTIVE_INST_VALU", 0) * 4 / (1024 * r["GRBM_GUI_ACTIVE"] / 8) if r.get("GRBM_GUI_ACTIVE") else 0
+        # wave64 VALU instructions x 2 cycles over the SIMD-cycles of the dispatch (1024 SIMDs, GRBM_GUI_ACTIVE counts
+        # each of the 8 XCDs).  SQ_ACTIVE_INST_VALU is NOT a busy-cycle count on gfx950: it equals SQ_INSTS_VALU.
+        busy = r.get("SQ_INSTS_VALU", 0) * 2 / (1024 * r["GRBM_GUI_ACTIVE"] / 8) if r.get("GRBM_GUI_ACTIVE") else 0
         f.write(f"| {k} | {r.get('avg_duration_ns', 0):.0f} | {r.get('dispatches', 0)} | {vpw:.0f} | {stall:.2f} | "
                 f"{wait:.2f} | {r.get('FETCH_SIZE', 0):.0f} | {r.get('WRITE_SIZE', 0):.0f} | {clk:.2f} | {busy:.2f} |\n")
 print(open(os.path.join(dst, f"{tag}_summary.md")).read())

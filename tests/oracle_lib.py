@@ -35,6 +35,7 @@ def lib():
         L.ora_leo_bits_for.argtypes = [ctypes.c_int]
         L.ora_leo_encode.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P]
         L.ora_leo_decode.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P]
+        L.ora_leo_decode_fft.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P]
         L.ora_leo_mul.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_uint]
         L.ora_leo_mul.restype = ctypes.c_uint
         L.ora_leo_skew.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -50,6 +51,7 @@ def lib():
                                                    ctypes.POINTER(ctypes.c_double)]
         L.ora_extend_commit_throughput.restype = ctypes.c_long
         L.ora_repair.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, P]
+        L.ora_repair_ex.argtypes = [ctypes.c_int, ctypes.c_size_t, P, P, P, P, P, P, ctypes.c_int]
         L.ora_gen_ods.argtypes = [ctypes.c_int, ctypes.c_uint64, P]
         _bind_inclusion(L)
         _LIB = L
@@ -94,13 +96,15 @@ def leo_encode(data: np.ndarray) -> np.ndarray:
     return par
 
 
-def leo_decode(shards: np.ndarray, present: np.ndarray):
-    """shards: (2k, L) with garbage where missing; returns (rc, repaired copy)."""
+def leo_decode(shards: np.ndarray, present: np.ndarray, fft: bool = False):
+    """shards: (2k, L) with garbage where missing; returns (rc, repaired copy).  fft=False: the Lagrange decoder
+    (independent check); fft=True: klauspost's Leopard reconstruct (error locators + IFFT/FFT)."""
     sh = np.ascontiguousarray(shards, np.uint8).copy()
     n, L = sh.shape
     pres = np.ascontiguousarray(present, np.uint8)
     rows = [sh[i] for i in range(n)]
-    rc = lib().ora_leo_decode(n // 2, L, _ptr_array(rows), _p(pres))
+    fn = lib().ora_leo_decode_fft if fft else lib().ora_leo_decode
+    rc = fn(n // 2, L, _ptr_array(rows), _p(pres))
     return rc, sh
 
 
@@ -176,14 +180,15 @@ def merkle_root(items) -> bytes:
     return out.tobytes()
 
 
-def repair(eds: np.ndarray, present: np.ndarray, row_roots: np.ndarray, col_roots: np.ndarray):
+def repair(eds: np.ndarray, present: np.ndarray, row_roots: np.ndarray, col_roots: np.ndarray, fft: bool = False):
+    """rsmt2d Repair restated (sequential).  fft selects the decoder as in leo_decode."""
     eds = np.ascontiguousarray(eds, np.uint8).copy()
     pres = np.ascontiguousarray(present, np.uint8).copy()
     w = row_roots.shape[0]
     ea = np.zeros(1, np.int32)
     ei = np.zeros(1, np.int32)
-    rc = lib().ora_repair(w // 2, eds.shape[1], _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots)),
-                          _p(np.ascontiguousarray(col_roots)), _p(ea), _p(ei))
+    rc = lib().ora_repair_ex(w // 2, eds.shape[1], _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots)),
+                             _p(np.ascontiguousarray(col_roots)), _p(ea), _p(ei), 1 if fft else 0)
     return rc, eds, pres, int(ea[0]), int(ei[0])
 
 

@@ -219,3 +219,30 @@ def test_oracle_matches_committed_digests():
         assert rc == 0 and dah.hex() == fx[ks]["dah"]
         assert hashlib.sha256(eds.tobytes()).hexdigest() == fx[ks]["eds_sha256"]
         assert hashlib.sha256(rr.tobytes() + cr.tobytes()).hexdigest() == fx[ks]["roots_sha256"]
+
+
+def test_leopard_reconstruct_matches_lagrange():
+    """ora_leo_decode_fft (klauspost's reconstruct restated: error locators, IFFT, formal derivative, FFT; the CPU
+    baseline's decoder) returns the same shards as the independent Lagrange decoder, FF8 and FF16, ragged k."""
+    rng = np.random.default_rng(5)
+    for k in (1, 2, 3, 8, 33, 128, 129, 300):
+        data = rng.integers(0, 256, (k, 64), dtype=np.uint8)
+        sh = np.concatenate([data, O.leo_encode(data)])
+        pres = np.zeros(2 * k, np.uint8)
+        pres[rng.permutation(2 * k)[:k]] = 1
+        bad = sh.copy()
+        bad[pres == 0] = 0x5A
+        rc1, a = O.leo_decode(bad, pres)
+        rc2, b = O.leo_decode(bad, pres, fft=True)
+        assert rc1 == rc2 == 0 and np.array_equal(a, sh) and np.array_equal(b, sh), k
+
+
+def test_repair_fft_decoder_matches_lagrange():
+    k, w = 16, 32
+    rc, eds, rr, cr, dah = O.extend_commit(O.gen_ods(k, 77))
+    pres = (np.random.default_rng(3).random(w * w) < 0.5).astype(np.uint8)
+    d = eds.copy()
+    d[pres == 0] = 0
+    r0 = O.repair(d, pres, rr, cr)
+    r1 = O.repair(d, pres, rr, cr, fft=True)
+    assert r0[0] == r1[0] == 0 and np.array_equal(r0[1], eds) and np.array_equal(r1[1], eds)
