@@ -442,16 +442,45 @@ def k512_measure(ctx, dev, reps=3):
            "kernels_ms": {n: round(ms / max(1, cnt), 3) for n, (ms, cnt) in prof.items()},
            "parity": "GF(2^16) unpinned by reference data (Lagrange-oracle checked)"}
     del eds, roots
-    ops = split.DeviceOps(ctx)
+    # config C5's split path behind the C ABI (cda_multi_extend_commit_split_device): one square over the devices of
+    # a handle.  On one GPU: G = 1 (the row slab is the column slab's top half, no exchange) and G = 8 replicas on
+    # this device (the 8-device plan with device copies for the RCCL exchange -- a rehearsal, not a scaling number)
+    want_dah = want[str(0xC0FFEE)]
     rows = ods[0].view(k, k, 512)
+    for G in (1, 8):
+        m = cda.MultiContext.replicas(dev.index, G)
+        rp = k // G
+        slabs = [rows[g * rp:(g + 1) * rp].contiguous() for g in range(G)]
+        torch.cuda.synchronize(dev)
+        ptrs = [sl.data_ptr() for sl in slabs]
+        m.extend_commit_split_device(k, ptrs)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            _, _, d = m.extend_commit_split_device(k, ptrs)
+        el = (time.perf_counter() - t0) / reps
+        if d.hex() != want_dah:
+            raise RuntimeError(f"split (G={G}) DAH differs from the committed digest")
+        prof = None
+        if G == 1:
+            c0 = m.context(0)
+            c0.profile_reset()
+            c0.profile_enable(True)
+            m.extend_commit_split_device(k, ptrs)
+            prof = {n: round(ms / max(1, cnt), 3) for n, (ms, cnt) in c0.profile_read().items()}
+            c0.profile_enable(False)
+        out[f"split_capi_G{G}_on_1gpu"] = {"ms_per_square": round(el * 1e3, 3), "dah_matches_golden": True,
+                                            **({"kernels_ms": prof} if prof else {})}
+        m.close()
+    ops = split.DeviceOps(ctx)
     split.extend_commit_split(ops, k, rows)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(reps):
         res = split.extend_commit_split(ops, k, rows)
     torch.cuda.synchronize(dev)
-    out["split_on_1gpu"] = {"ms_per_square": round((time.perf_counter() - t0) * 1e3 / reps, 3),
-                            "dah_matches_block_path": res.dah == dah[0].cpu().numpy().tobytes()}
+    out["split_py_on_1gpu"] = {"ms_per_square": round((time.perf_counter() - t0) * 1e3 / reps, 3),
+                               "dah_matches_golden": res.dah.hex() == want_dah,
+                               "note": "cda/split.py over torch.distributed (world 1), the cross-process form"}
     return out
 
 

@@ -51,7 +51,8 @@ EXPORTS = [
     "cda_blob_commitments", "cda_merkle_roots", "cda_extend_commit_nodes", "cda_share_inclusion_proof",
     "cda_host_alloc", "cda_host_free", "cda_multi_init", "cda_multi_free", "cda_multi_device_count",
     "cda_multi_context", "cda_multi_device", "cda_multi_extend_commit_batch", "cda_build_ods_device",
-    "cda_construct_extend_commit",
+    "cda_construct_extend_commit", "cda_multi_extend_commit_split", "cda_multi_extend_commit_split_device",
+    "cda_multi_init_replicas",
 ]
 
 
@@ -132,6 +133,9 @@ def lib():
                 "cda_multi_context": (P, [P, I32]),
                 "cda_multi_device": (I32, [P, I32]),
                 "cda_multi_extend_commit_batch": (I32, [P, U32, U32, P, P, P, P, P, P]),
+                "cda_multi_extend_commit_split": (I32, [P, U32, P, P, P, P, P, P]),
+                "cda_multi_extend_commit_split_device": (I32, [P, U32, P, P, P, P, P]),
+                "cda_multi_init_replicas": (I32, [I32, U32, ctypes.POINTER(P)]),
                 "cda_build_ods_device": (I32, [P, U32, U32, P, P, U64, P, U32, P, P]),
                 "cda_construct_extend_commit": (I32, [P, U32, U32, P, P, U64, P, U32, P, P, P, P, P, P]),
             }
@@ -177,9 +181,9 @@ class Context:
         self.device = device
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and not getattr(self, "_borrowed", False):  # a MultiContext's view: not ours
             lib().cda_free(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -494,14 +498,63 @@ class PinnedBuffer:
 
 
 class MultiContext:
-    """cda_multi: one handle over several GPUs of this process (device mask; 0 = all visible)."""
+    """cda_multi: one handle over several GPUs of this process (device mask; 0 = all visible).
+    MultiContext.replicas(device, n): n contexts on one device whose split exchanges are device copies."""
 
-    def __init__(self, device_mask=0):
+    def __init__(self, device_mask=0, _handle=None):
+        if _handle is not None:
+            self._h = _handle
+            return
         h = ctypes.c_void_p()
         rc = lib().cda_multi_init(device_mask, ctypes.byref(h))
         if rc != OK:
             raise CdaError(rc, "cda_multi_init failed")
         self._h = h
+
+    @classmethod
+    def replicas(cls, device, count):
+        h = ctypes.c_void_p()
+        rc = lib().cda_multi_init_replicas(device, count, ctypes.byref(h))
+        if rc != OK:
+            raise CdaError(rc, "cda_multi_init_replicas failed")
+        return cls(_handle=h)
+
+    def context(self, i):
+        """Context view of device i's cda_ctx (owned by this handle)."""
+        c = Context.__new__(Context)
+        c._h = ctypes.c_void_p(lib().cda_multi_context(self._h, i))
+        c.device = lib().cda_multi_device(self._h, i)
+        c._borrowed = True
+        return c
+
+    def extend_commit_split(self, ods, want_eds=True):
+        """ONE k x k square (ods: (k*k, 512) uint8) split over the handle's devices (cda_multi_extend_commit_split).
+        Returns (eds or None, row_roots, col_roots, dah bytes)."""
+        ods = np.ascontiguousarray(ods, np.uint8)
+        count = ods.shape[0]
+        k = int(round(count ** 0.5))
+        if k * k != count or ods.shape[1] != SHARE_SIZE:
+            raise CdaError(E_ARG, "ods must be (k*k, 512)")
+        eds = np.empty((4 * k * k, SHARE_SIZE), np.uint8) if want_eds else None
+        rr = np.zeros((2 * k, NODE_SIZE), np.uint8)
+        cr = np.zeros((2 * k, NODE_SIZE), np.uint8)
+        dah = np.zeros(32, np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_multi_extend_commit_split(self._h, k, _p(ods), _p(eds), _p(rr), _p(cr), _p(dah),
+                                                 ctypes.byref(err))
+        _check(rc, err, self.context(0))
+        return eds, rr, cr, dah.tobytes()
+
+    def extend_commit_split_device(self, k, slab_ptrs):
+        """The split with device g's ODS rows already at device pointer slab_ptrs[g]; returns (rr, cr, dah)."""
+        arr = (ctypes.c_void_p * len(slab_ptrs))(*slab_ptrs)
+        rr = np.zeros((2 * k, NODE_SIZE), np.uint8)
+        cr = np.zeros((2 * k, NODE_SIZE), np.uint8)
+        dah = np.zeros(32, np.uint8)
+        err = ErrInfo()
+        rc = lib().cda_multi_extend_commit_split_device(self._h, k, arr, _p(rr), _p(cr), _p(dah), ctypes.byref(err))
+        _check(rc, err, self.context(0))
+        return rr, cr, dah.tobytes()
 
     @property
     def device_count(self):

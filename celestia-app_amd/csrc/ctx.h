@@ -48,6 +48,10 @@ struct cda_ctx {
     size_t cap = 0;
   };
   Buf ods, eds, leaf, scratch, roots, dah, status, plan, payload;
+  // one square split over devices (split.cpp): this device's slab, row / column slabs, leaf records, send blocks,
+  // tree scratch, per-device results (meta) and, on the first device, the gathered results
+  Buf sp_ods, sp_R, sp_LR, sp_S, sp_C, sp_LC, sp_scratch, sp_meta, sp_gather;
+  hipEvent_t sp_ev[2] = {};  // replicas transport: sender-side "ready" events
   // repair: device root table + per-sweep descriptors, and their pinned host staging
   Buf rdesc, rstage;
   // pinned staging rings for cda_repair's large copies of caller (pageable) memory, one per direction
@@ -98,6 +102,15 @@ int staged_d2h(cda_ctx* c, void* h_dst, const void* d_src, size_t n, hipStream_t
 void free_staging(cda_ctx* c);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
+// split_kernels.hip
+int launch_region_leaf(const uint8_t* d_cells, long long cell_pitch, int r0, int c0, int nr, int nc, int k,
+                       void* d_recs, long long rec_pitch, unsigned long long* d_status, bool row_order, hipStream_t s);
+int launch_records_col_order(const void* d_recs, long long rec_pitch, int nr, int c0, int nc, int k,
+                             unsigned long long* d_status, hipStream_t s);
+void free_split_comm(cda_multi* m);  // split.cpp
+int launch_tree_roots(const void* d_leaves, unsigned long long t_stride, unsigned long long i_stride, int log2n,
+                      uint32_t ntrees, bool tree_fastest, void* d_scratch, void* d_roots, unsigned long long r_stride,
+                      hipStream_t s);
 
 // ---- exception barrier of the C ABI ----
 // No C++ exception may cross an extern "C" entry point: under cgo it reaches std::terminate inside the Go node,
@@ -130,6 +143,9 @@ struct ThreadJoiner {
       if (t->joinable()) t->join();
   }
 };
+
+// One handle over several contexts (host_pipeline.cpp: block batches; split.cpp: one square split over them).
+struct SplitComm;  // split.cpp: RCCL communicators of the handle
 
 // Synchronous entry points (work on c->stream): ordered after any device-resident enqueue.
 struct Lock {
@@ -164,3 +180,12 @@ struct DevLock {
 };
 
 }  // namespace cda
+
+struct cda_multi {
+  std::vector<cda_ctx*> ctx;
+  std::vector<int> devices;
+  bool replicas = false;              // every context on one device (cda_multi_init_replicas): split exchanges are
+                                      // device copies instead of RCCL (tests, rehearsal of G > 1 on one GPU)
+  std::mutex split_mu;                // one split at a time per handle
+  cda::SplitComm* comm = nullptr;     // RCCL communicators (created by the first split with G > 1)
+};

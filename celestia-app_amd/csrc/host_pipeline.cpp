@@ -259,10 +259,7 @@ int cda_host_free(cda_ctx* c, void* p) {
 }
 
 // ---- multi-device batch ----------------------------------------------------------------------
-struct cda_multi {
-  std::vector<cda_ctx*> ctx;
-  std::vector<int> devices;
-};
+// (struct cda_multi: ctx.h)
 
 int cda_multi_init(uint32_t device_mask, cda_multi** out) {
   CDA_API_TRY
@@ -294,6 +291,7 @@ int cda_multi_init(uint32_t device_mask, cda_multi** out) {
 
 void cda_multi_free(cda_multi* m) {
   if (!m) return;
+  free_split_comm(m);
   for (auto* c : m->ctx) cda_free(c);
   delete m;
 }

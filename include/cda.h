@@ -134,6 +134,24 @@ int cda_multi_extend_commit_batch(cda_multi* m, uint32_t k, uint32_t nblocks, co
                                   uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                                   cda_err_info* err);
 
+/* ---- one square split over the handle's devices ----
+ * da.ExtendShares + NewDataAvailabilityHeader (pkg/da/data_availability_header.go:44-75) of ONE k x k square
+ * (k up to 512: appconsts/testground SquareSizeUpperBound, pkg/appconsts/testground/app_consts.go:8) over the G
+ * devices of `m` (G a power of two dividing k): device g row-encodes ODS rows [g k/G, (g+1) k/G), one RCCL exchange
+ * (ncclSend / ncclRecv pairs in one group, communicators from ncclCommInitAll) hands every device the top half of
+ * its 2k/G columns with their leaf records, each device column-encodes and roots its columns and the bottom rows'
+ * subtrees over them, and device 0 folds those and hashes the DAH.  Outputs and errors as cda_extend_commit
+ * (ods: k*k*512 bytes row-major; eds_or_null: 4k^2*512, gathered from the devices). */
+int cda_multi_extend_commit_split(cda_multi* m, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null,
+                                  uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err);
+/* The same with the ODS already on the devices: d_ods_slabs[g] = device memory of device g holding ODS rows
+ * [g k/G, (g+1) k/G) (k/G * k * 512 bytes).  The EDS stays on the devices (in the handle's workspace). */
+int cda_multi_extend_commit_split_device(cda_multi* m, uint32_t k, const void* const* d_ods_slabs, uint8_t* row_roots,
+                                         uint8_t* col_roots, uint8_t* dah, cda_err_info* err);
+/* A handle of `count` contexts on ONE device whose split exchanges are device-to-device copies instead of RCCL:
+ * the same plan and kernels for G = 2, 4, 8 on a single GPU (tests, rehearsal).  Free with cda_multi_free. */
+int cda_multi_init_replicas(int device, uint32_t count, cda_multi** out);
+
 /* Device-resident form (pointers are device memory of this ctx's GPU; `stream`
  * is a hipStream_t or NULL for the null stream).  Asynchronous: returns after
  * enqueueing; namespace-order errors are reported into the device word
