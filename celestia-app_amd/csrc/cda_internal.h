@@ -110,6 +110,16 @@ int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t
 int launch_build_ods(const cda_share_segment* d_segs, int nseg, const uint8_t* d_data, const uint32_t* d_reserved,
                      uint32_t nshares, void* d_ods, hipStream_t s);
 
+struct TreeSpec {  // a set of trees for launch_tree_roots
+  const void* leaves;
+  unsigned long long t_stride, i_stride;  // leaf i of tree t = leaves[t * t_stride + i * i_stride] (96-B records)
+  uint32_t ntrees;
+  bool tree_fastest;  // node-major inner levels (consecutive trees on consecutive lanes)
+  void* scratch;      // ntrees * n records
+  void* roots;
+  unsigned long long r_stride;
+};
+
 // profiling hook implemented by the engine
 struct ProfScope {
   void* ctx;

@@ -108,9 +108,7 @@ int launch_region_leaf(const uint8_t* d_cells, long long cell_pitch, int r0, int
 int launch_records_col_order(const void* d_recs, long long rec_pitch, int nr, int c0, int nc, int k,
                              unsigned long long* d_status, hipStream_t s);
 void free_split_comm(cda_multi* m);  // split.cpp
-int launch_tree_roots(const void* d_leaves, unsigned long long t_stride, unsigned long long i_stride, int log2n,
-                      uint32_t ntrees, bool tree_fastest, void* d_scratch, void* d_roots, unsigned long long r_stride,
-                      hipStream_t s);
+int launch_tree_roots(const TreeSpec* spec, int nsets, int log2n, hipStream_t s);
 
 // ---- exception barrier of the C ABI ----
 // No C++ exception may cross an extern "C" entry point: under cgo it reaches std::terminate inside the Go node,

@@ -76,7 +76,7 @@ int ensure_split(cda_ctx* c, const Plan& p, int g) {
   if ((rc = ensure(c, c->sp_ods, (size_t)p.rp * p.k * p.S)) || (rc = ensure(c, c->sp_C, (size_t)p.w * p.cp * p.S)) ||
       (rc = ensure(c, c->sp_LC, (size_t)p.w * p.cp * p.R)) ||
       (rc = ensure(c, c->sp_scratch,
-                   std::max({(size_t)p.w * p.rp, (size_t)p.w * p.cp, (size_t)p.k * p.G}) * p.R)) ||
+                   std::max({(size_t)p.w * (p.rp + p.cp), (size_t)p.k * p.cp, (size_t)p.k * p.G}) * p.R)) ||
       (rc = ensure(c, c->sp_meta, p.meta_recs() * p.R)))
     return rc;
   if (p.G > 1) {
@@ -143,12 +143,6 @@ int row_pass(cda_ctx* c, const Plan& p, uint32_t g, const uint8_t* d_slab) {
     if (launch_region_leaf(R, (long long)p.w * p.S, (int)r0, 0, (int)p.rp, (int)p.w, (int)p.k, LR, p.w, st, true, s))
       return CDA_E_DEVICE;
   }
-  {
-    ProfScope ps(c, "split_tree_rows", s);
-    int L = 0;
-    while ((1u << L) < p.w) L++;
-    if (launch_tree_roots(LR, p.w, 1, L, p.rp, false, c->sp_scratch.p, meta, 1, s)) return CDA_E_DEVICE;
-  }
   if (p.G > 1) {  // block h = this device's rows x h's columns: shares and leaf records, packed contiguous
     uint8_t* C = (uint8_t*)c->sp_C.p;
     uint8_t* LC = (uint8_t*)c->sp_LC.p;
@@ -199,19 +193,24 @@ int col_pass(cda_ctx* c, const Plan& p, uint32_t h) {
   int L = 0, Lc = 0;
   while ((1u << L) < p.w) L++;
   while ((1u << Lc) < p.cp) Lc++;
-  {
-    ProfScope ps(c, "split_tree_cols", s);
-    if (launch_tree_roots(LC, 1, p.cp, L, p.cp, true, c->sp_scratch.p, meta + (size_t)p.rp * p.R, 1, s))
-      return CDA_E_DEVICE;
+  {  // the roots of this device's top rows (row leaf records LR, tree-major) and of its columns (LC, node-major)
+     // in one launch sequence, so neither set's thin top levels run alone
+    ProfScope ps(c, "split_trees", s);
+    uint8_t* sc = (uint8_t*)c->sp_scratch.p;
+    const TreeSpec sets[2] = {
+        {row_recs(c, p), p.w, 1, p.rp, false, sc, meta, 1},
+        {LC, 1, p.cp, p.cp, true, sc + (size_t)p.rp * p.w * p.R, meta + (size_t)p.rp * p.R, 1}};
+    if (launch_tree_roots(sets, 2, L, s)) return CDA_E_DEVICE;
   }
-  {
+  {  // bottom rows: the subtree over this device's cp columns
     ProfScope ps(c, "split_tree_bottom", s);
     uint8_t* sub = meta + ((size_t)p.rp + p.cp) * p.R;
     const uint8_t* leaves = LC + (size_t)p.k * p.cp * p.R;
     if (Lc == 0) {
       HIPC(c, hipMemcpyAsync(sub, leaves, (size_t)p.k * p.R, hipMemcpyDeviceToDevice, s), "copy");
-    } else if (launch_tree_roots(leaves, p.cp, 1, Lc, p.k, false, c->sp_scratch.p, sub, 1, s)) {
-      return CDA_E_DEVICE;
+    } else {
+      const TreeSpec set{leaves, p.cp, 1, p.k, false, c->sp_scratch.p, sub, 1};
+      if (launch_tree_roots(&set, 1, Lc, s)) return CDA_E_DEVICE;
     }
   }
   return CDA_OK;
@@ -236,7 +235,8 @@ int finish_pass(cda_ctx* c0, const Plan& p) {
     int Lg = 0;
     while ((1u << Lg) < p.G) Lg++;
     ProfScope ps(c0, "split_fold", s);
-    if (launch_tree_roots(sub, 1, mr, Lg, p.k, true, c0->sp_scratch.p, bottom, 1, s)) return CDA_E_DEVICE;
+    const TreeSpec set{sub, 1, mr, p.k, true, c0->sp_scratch.p, bottom, 1};
+    if (launch_tree_roots(&set, 1, Lg, s)) return CDA_E_DEVICE;
   }
   ProfScope ps(c0, "dah", s);
   const int lr = launch_dah(fin, dah, (int)(4 * p.k), 1, s);
@@ -402,19 +402,29 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
   } else {
     for (uint32_t g = 0; g < G; g++) slab[g] = (const uint8_t*)d_slabs[g];
   }
-  for (uint32_t g = 0; g < G; g++) {
-    (void)hipSetDevice(m->ctx[g]->device);
-    TRY(row_pass(m->ctx[g], p, g, slab[g]));
-  }
-  TRY(exchange(m, p));
-  for (uint32_t h = 0; h < G; h++) {
-    (void)hipSetDevice(m->ctx[h]->device);
-    TRY(col_pass(m->ctx[h], p, h));
-  }
-  TRY(gather(m, p));
   cda_ctx* c0 = m->ctx[0];
-  (void)hipSetDevice(c0->device);
-  TRY(finish_pass(c0, p));
+  if (G == 1) {
+    // one device: its column slab is the whole 2k x 2k EDS, so the split is the block pipeline itself (RS rows and
+    // columns, leaf hashing shared by row and column trees, all 4k trees, DAH) into the result area
+    uint8_t* gat = (uint8_t*)c0->sp_gather.p;
+    uint8_t* fin = gat + p.meta_recs() * p.R;
+    unsigned long long* st = (unsigned long long*)(gat + (p.meta_recs() - 1) * p.R);
+    HIPC(c0, hipMemsetAsync(st, 0xFF, 8, c0->stream), "memset");
+    TRY(enqueue_pipeline(c0, k, 1, slab[0], (uint8_t*)c0->sp_C.p, fin, fin + 4 * (size_t)k * p.R, st, c0->stream));
+  } else {
+    for (uint32_t g = 0; g < G; g++) {
+      (void)hipSetDevice(m->ctx[g]->device);
+      TRY(row_pass(m->ctx[g], p, g, slab[g]));
+    }
+    TRY(exchange(m, p));
+    for (uint32_t h = 0; h < G; h++) {
+      (void)hipSetDevice(m->ctx[h]->device);
+      TRY(col_pass(m->ctx[h], p, h));
+    }
+    TRY(gather(m, p));
+    (void)hipSetDevice(c0->device);
+    TRY(finish_pass(c0, p));
+  }
   // results: 4k roots + DAH + G status words from device 0; the EDS from where each part lives
   const size_t mr = p.meta_recs();
   std::vector<uint8_t> fin(4 * (size_t)k * p.R + 32);
@@ -424,7 +434,9 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
        "D2H");
   HIPC(c0, hipMemcpy2DAsync(st.data(), 8, gat + (mr - 1) * p.R, mr * p.R, 8, G, hipMemcpyDeviceToHost, c0->stream),
        "D2H");
-  if (eds) {
+  if (eds && G == 1) {
+    HIPC(c0, hipMemcpyAsync(eds, c0->sp_C.p, (size_t)p.w * p.w * p.S, hipMemcpyDeviceToHost, c0->stream), "D2H");
+  } else if (eds) {
     for (uint32_t g = 0; g < G; g++) {  // top rows from each row slab, bottom half from each column slab
       cda_ctx* c = m->ctx[g];
       (void)hipSetDevice(c->device);

@@ -61,32 +61,39 @@ __global__ void __launch_bounds__(256) records_col_order_kernel(const uint4* __r
     atomicMin(status, ((unsigned long long)CDA_AXIS_COL << 40) | ((unsigned long long)c << 20) | (unsigned)(r + 1));
 }
 
-// Levels of a set of trees, M levels per launch (the nmt_levels_kernel scheme with free strides): node i of tree t
-// at level l is record lv[l].p[t * t_stride + i * i_stride].  A thread owns one output node and computes its
-// subtree; tree_fastest puts consecutive trees on consecutive lanes (node-major layouts).
+// Levels of up to two sets of trees with the same depth, M levels per launch (the nmt_levels_kernel scheme with
+// free strides): node i of tree t at level l is record lv[l].p[t * t_stride + i * i_stride].  A thread owns one
+// output node and computes its subtree; tree_fastest puts consecutive trees on consecutive lanes (node-major
+// layouts).  Both sets share a launch so the thin top levels of one set are not launched alone.
 struct TreeLevel {
   uint4* p;
   unsigned long long t_stride, i_stride;
 };
-struct TreeSet {
-  TreeLevel lv[4];
+struct TreeSets {
+  TreeLevel lv[2][4];
+  uint32_t ntrees[2];
+  int tree_fastest[2];
 };
 
 __device__ __forceinline__ uint4* tree_rec(const TreeLevel& d, unsigned t, unsigned i) {
   return d.p + (t * d.t_stride + i * d.i_stride) * 6;
 }
 
-__global__ void __launch_bounds__(256) tree_levels_kernel(TreeSet ts, int log2n_out, int M, uint32_t ntrees,
-                                                          int tree_fastest) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= ntrees << log2n_out) return;
-  const unsigned t = tree_fastest ? gid % ntrees : gid >> log2n_out;
-  const unsigned j = tree_fastest ? gid / ntrees : gid & ((1u << log2n_out) - 1);
+__global__ void __launch_bounds__(256) tree_levels_kernel(TreeSets ts, int log2n_out, int M, uint32_t total0,
+                                                          uint32_t total) {
+  uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int set = gid >= total0;
+  if (set) gid -= total0;
+  const uint32_t ntrees = ts.ntrees[set];
+  const unsigned t = ts.tree_fastest[set] ? gid % ntrees : gid >> log2n_out;
+  const unsigned j = ts.tree_fastest[set] ? gid / ntrees : gid & ((1u << log2n_out) - 1);
+  const TreeLevel* lv = ts.lv[set];
   for (int q = 1; q <= M; q++) {
     const unsigned cnt = 1u << (M - q);
     for (unsigned u = 0; u < cnt; u++) {
       const unsigned i = j * cnt + u;
-      hash_node_mem(tree_rec(ts.lv[q - 1], t, 2 * i), tree_rec(ts.lv[q - 1], t, 2 * i + 1), tree_rec(ts.lv[q], t, i));
+      hash_node_mem(tree_rec(lv[q - 1], t, 2 * i), tree_rec(lv[q - 1], t, 2 * i + 1), tree_rec(lv[q], t, i));
     }
     if (q < M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -113,44 +120,50 @@ int launch_records_col_order(const void* d_recs, long long rec_pitch, int nr, in
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// ntrees trees of n = 2^log2n leaves (leaf i of tree t = leaves[t * t_stride + i * i_stride]) -> roots[t * r_stride].
-// Inner levels go to d_scratch (ntrees * n records suffice), tree-major unless tree_fastest (then node-major).
-int launch_tree_roots(const void* d_leaves, unsigned long long t_stride, unsigned long long i_stride, int log2n,
-                      uint32_t ntrees, bool tree_fastest, void* d_scratch, void* d_roots, unsigned long long r_stride,
-                      hipStream_t s) {
-  if (ntrees == 0) return 0;
+// Up to two sets of trees of n = 2^log2n leaves each: set q has spec[q].ntrees trees, leaf i of tree t at
+// leaves[t * t_stride + i * i_stride], root to roots[t * r_stride]; inner levels in its own scratch (ntrees * n
+// records suffice), tree-major unless tree_fastest (then node-major).
+int launch_tree_roots(const TreeSpec* spec, int nsets, int log2n, hipStream_t s) {
+  if (nsets < 1 || nsets > 2) return -2;
   if (log2n == 0) return -2;  // a one-leaf tree's root is the leaf record: the caller copies it
   const int L = log2n;
-  auto desc = [&](int l) {
+  auto desc = [&](const TreeSpec& sp, int l) {
     TreeLevel d{};
     const unsigned long long n = 1ull << (L - l);
     if (l == 0) {
-      d.p = (uint4*)d_leaves;
-      d.t_stride = t_stride;
-      d.i_stride = i_stride;
+      d.p = (uint4*)sp.leaves;
+      d.t_stride = sp.t_stride;
+      d.i_stride = sp.i_stride;
     } else if (l == L) {
-      d.p = (uint4*)d_roots;
-      d.t_stride = r_stride;
+      d.p = (uint4*)sp.roots;
+      d.t_stride = sp.r_stride;
       d.i_stride = 0;
     } else {
       unsigned long long off = 0;
-      for (int q = 1; q < l; q++) off += (unsigned long long)ntrees << (L - q);
-      d.p = (uint4*)d_scratch + off * 6;
-      d.t_stride = tree_fastest ? 1 : n;
-      d.i_stride = tree_fastest ? ntrees : 1;
+      for (int q = 1; q < l; q++) off += (unsigned long long)sp.ntrees << (L - q);
+      d.p = (uint4*)sp.scratch + off * 6;
+      d.t_stride = sp.tree_fastest ? 1 : n;
+      d.i_stride = sp.tree_fastest ? sp.ntrees : 1;
     }
     return d;
   };
   for (int l_in = 0; l_in < L;) {
     int M = std::min(2, L - l_in);
     if (L - l_in == 3) M = 3;
-    TreeSet ts{};
-    for (int q = 0; q <= M; q++) ts.lv[q] = desc(l_in + q);
+    TreeSets ts{};
+    for (int q = 0; q < nsets; q++) {
+      for (int u = 0; u <= M; u++) ts.lv[q][u] = desc(spec[q], l_in + u);
+      ts.ntrees[q] = spec[q].ntrees;
+      ts.tree_fastest[q] = spec[q].tree_fastest ? 1 : 0;
+    }
     const int log2n_out = L - (l_in + M);
-    const uint32_t total = ntrees << log2n_out;
-    hipLaunchKernelGGL(tree_levels_kernel, dim3((total + 255) / 256), dim3(256), 0, s, ts, log2n_out, M, ntrees,
-                       tree_fastest ? 1 : 0);
-    if (hipGetLastError() != hipSuccess) return -1;
+    const uint32_t total0 = spec[0].ntrees << log2n_out;
+    const uint32_t total = total0 + (nsets > 1 ? spec[1].ntrees << log2n_out : 0);
+    if (total) {
+      hipLaunchKernelGGL(tree_levels_kernel, dim3((total + 255) / 256), dim3(256), 0, s, ts, log2n_out, M, total0,
+                         total);
+      if (hipGetLastError() != hipSuccess) return -1;
+    }
     l_in += M;
   }
   return 0;

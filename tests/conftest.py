@@ -12,6 +12,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libcda on the device)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """PyTorch ships its own HIP / HSA runtime (torch/lib) while libcda links /opt/rocm's; with both in one process
+    torch's must initialise first, or torch.cuda reports "No HIP GPUs are available" (libcda works either way).
+    A Go node has no torch: this concerns the Python tests and tools only."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 @pytest.fixture(scope="session")
 def ctx():
     import cda
