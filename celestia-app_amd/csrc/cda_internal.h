@@ -52,6 +52,10 @@ int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d
                      int ncw, int k, int shard_len, hipStream_t s);
 int launch_rs_encode8(const RsJob& job, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
+// register-resident GF(2^16) encoder for k = 512 (rs16_kernels.hip)
+bool rs16_reg_eligible(const RsJob& j);
+int rs16_reg_init(int device);
+int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t s);
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,
                      hipStream_t s);
 int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int nblocks, int level, hipStream_t s);

@@ -1,0 +1,468 @@
+// rs16_kernels.hip — register-resident Leopard GF(2^16) encoder for m = 512 (k = 512, config C5: the testground
+// square, pkg/appconsts/testground/app_consts.go:8).
+//
+// Reference: klauspost/reedsolomon v1.12.1 leopardFF16 encode as called by rsmt2d LeoRSCodec for 2k > 256
+// (upstream, pinned go.mod:153): work = data at points m..2m-1; IFFT-DIT with
+// skew[m - 1 + s0 + D], then FFT-DIT with skew[s0 + D - 1]; radix-2 layers d = log2 D (rs_kernels.hip header).
+//
+// Design.  One workgroup holds ONE whole codeword in registers: 512 positions x 512-B shards = 256 KiB = 16 waves x
+// 64 lanes x 64 VGPRs.  A lane owns one 64-B unit of 4 positions (unit = 32 GF(2^16) elements bit-sliced into 16
+// plane words, standard polynomial basis of GF(2)[x]/(x^16+x^5+x^3+x^2+1), as the LDS encoder):
+//   lane bits 0..2 = unit u (bytes [64u, 64u + 64) of every shard: 8 lanes read a whole 512-B shard),
+//   lane bits 3, 4, 5 = three position bits (A3, A4, A5), register slot bits R0, R1 = two position bits,
+//   wave bits W0..W3 = four position bits.
+// A layer's butterfly bit is always moved into a register slot, so every butterfly is two register sets of one
+// lane.  The layouts (position bit p0..p8 -> slot) and the moves between them:
+//   LA  p0:R0 p1:R1 p2:A5 p3:A4 p4:A3 p5..p8:W0..W3   IFFT d = 0, 1          (load)  / FFT d = 1, 0   (store)
+//   LB  p2:R0 p3:R1 p0:A5 p1:A4                        IFFT d = 2             / FFT d = 2
+//       (LA <-> LB: v_permlane32_swap / v_permlane16_swap, one instruction per register pair and plane)
+//   LC  p4:R0 p3:R1 p2:A3                              IFFT d = 3, 4          / FFT d = 4, 3
+//       (LB <-> LC: DPP row_ror:8 = lane ^ 8, and two v_bitop3 selects)
+//   LD  p5:R0 p6:R1 p4:W0 p3:W1                        IFFT d = 5, 6          / FFT d = 6, 5
+//   LE  p7:R0 p8:R1 p5:W2 p6:W3                        IFFT d = 7, 8, FFT d = 8, 7
+//       (LC <-> LD <-> LE: register bits <-> wave bits through LDS, 2 rounds of 8 planes, 128 KiB)
+// A layer constant depends on the position bits above d.  When they all sit in registers it is a compile-time
+// value and the multiply is its 16x16 GF(2) matrix as a straight v_bitop3 XOR3 program (~64 VALU); when some sit
+// in wave bits it is wave-uniform (runtime: scalar branches on its 16 bits); when some sit in lane bits (d <= 2) it
+// is per lane (16 lane masks x 16 planes, v_bitop3).  The old LDS encoder paid the per-lane form on 12 of 18 layers
+// and one LDS round trip + barrier per layer; here 6 of 18 layers are per-lane and the state crosses LDS 4 times.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cda_internal.h"
+#include "gf16_const.h"
+#include "gf_slice.h"
+
+namespace cda {
+
+namespace r16 {
+
+constexpr int L = 9, M = 1 << L;
+
+// ---- compile-time GF(2^16) matrices -------------------------------------------------------------------------------
+constexpr unsigned xtime16c(unsigned v) {
+  v <<= 1;
+  return (v & 0x10000u) ? (v ^ 0x1002Du) : v;
+}
+// row i of the matrix of y -> c*y: bit j = bit i of c * x^j
+constexpr unsigned mul_row(unsigned c, int i) {
+  unsigned row = 0, col = c;
+  for (int j = 0; j < 16; j++) {
+    row |= ((col >> i) & 1u) << j;
+    col = xtime16c(col);
+  }
+  return row;
+}
+// row i of a basis-change matrix given by its columns
+constexpr uint16_t kPhi[16] = {0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+                               0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E};
+constexpr uint16_t kPhiInv[16] = {0x0001, 0x4690, 0x65D8, 0x62D0, 0x5734, 0x45F0, 0x53B8, 0x1E38,
+                                  0x7CAE, 0x4E38, 0x6708, 0xC25C, 0x7A64, 0x9EAC, 0x1124, 0x523A};
+template <bool INV>
+constexpr unsigned basis_row(int i) {
+  unsigned row = 0;
+  for (int j = 0; j < 16; j++) row |= (unsigned)(((INV ? kPhiInv[j] : kPhi[j]) >> i) & 1u) << j;
+  return row;
+}
+
+// acc ^ XOR of Y[j] for the set bits j of ROW, two terms per v_bitop3 (XOR3)
+template <unsigned ROW, int J, int PEND>
+__device__ __forceinline__ uint32_t fold_row(uint32_t acc, const uint32_t (&Y)[16]) {
+  if constexpr (J == 16) {
+    if constexpr (PEND >= 0)
+      return acc ^ Y[PEND];
+    else
+      return acc;
+  } else if constexpr (((ROW >> J) & 1u) != 0) {
+    if constexpr (PEND < 0)
+      return fold_row<ROW, J + 1, J>(acc, Y);
+    else
+      return fold_row<ROW, J + 1, -1>(__builtin_amdgcn_bitop3_b32(acc, Y[PEND], Y[J], 0x96), Y);
+  } else {
+    return fold_row<ROW, J + 1, PEND>(acc, Y);
+  }
+}
+// X ^= C * Y, C a compile-time constant (0 = nothing)
+template <unsigned C, int I = 0>
+__device__ __forceinline__ void muladd_const(uint32_t (&X)[16], const uint32_t (&Y)[16]) {
+  if constexpr (C != 0 && I < 16) {
+    X[I] = fold_row<mul_row(C, I), 0, -1>(X[I], Y);
+    muladd_const<C, I + 1>(X, Y);
+  }
+}
+// V = Phi * V (INV = false: Leopard's Cantor coordinates -> standard basis; true: back)
+template <bool INV, int I = 0>
+__device__ __forceinline__ void basis_rows(uint32_t (&O)[16], const uint32_t (&V)[16]) {
+  if constexpr (I < 16) {
+    O[I] = fold_row<basis_row<INV>(I), 0, -1>(0u, V);
+    basis_rows<INV, I + 1>(O, V);
+  }
+}
+template <bool INV>
+__device__ __forceinline__ void change_basis(uint32_t (&V)[16]) {
+  uint32_t O[16];
+  basis_rows<INV>(O, V);
+#pragma unroll
+  for (int i = 0; i < 16; i++) V[i] = O[i];
+}
+
+__device__ __forceinline__ void xtime16(uint32_t (&T)[16]) {  // T *= x; x^16 = x^5 + x^3 + x^2 + 1
+  const uint32_t t = T[15];
+#pragma unroll
+  for (int i = 15; i > 0; i--) T[i] = T[i - 1];
+  T[0] = t;
+  T[2] ^= t;
+  T[3] ^= t;
+  T[5] ^= t;
+}
+// X ^= c * Y, c wave-uniform.  The bit tests are made to look lane-divergent (c copied into an opaque VGPR): the
+// compiler then guards each 16-XOR block with the exec mask, updating X in place, and skips the block with
+// s_cbranch_execz when the bit is clear.  As a scalar branch it renamed X in the taken block and paid 16 v_mov on the
+// other path, i.e. 16 VALU per bit either way.
+__device__ __forceinline__ void muladd_uniform(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
+  uint32_t cv = c;
+  asm volatile("" : "+v"(cv));
+  uint32_t T[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) T[j] = Y[j];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if ((cv >> i) & 1u) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) X[j] ^= T[j];
+    }
+    if (i < 15) xtime16(T);
+  }
+}
+// X ^= c * Y, c per lane (16 lane masks)
+__device__ __forceinline__ void muladd_lane(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
+  uint32_t T[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) T[j] = Y[j];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe(c, i, 1);  // -1 if bit i of c, else 0
+#pragma unroll
+    for (int j = 0; j < 16; j++) X[j] = __builtin_amdgcn_bitop3_b32(X[j], T[j], mk, 0x78);  // X ^ (T & mk)
+    if (i < 15) xtime16(T);
+  }
+}
+
+// ---- layouts -------------------------------------------------------------------------------------------------------
+// slot codes: 0, 1 = register bits R0, R1; 3, 4, 5 = lane bits; 8 + i = wave bit i
+struct Lay {
+  int s[L];
+};
+constexpr Lay LA{{0, 1, 5, 4, 3, 8, 9, 10, 11}};
+constexpr Lay LB{{5, 4, 0, 1, 3, 8, 9, 10, 11}};
+constexpr Lay LC{{5, 4, 3, 1, 0, 8, 9, 10, 11}};
+constexpr Lay LD{{5, 4, 3, 9, 8, 0, 1, 10, 11}};
+constexpr Lay LE{{5, 4, 3, 9, 8, 10, 11, 0, 1}};
+
+// position bits of register slot r under layout Y, and the masks of the lane / wave parts
+constexpr int pos_r(const Lay& Y, int r) {
+  int p = 0;
+  for (int b = 0; b < L; b++)
+    if (Y.s[b] < 2 && ((r >> Y.s[b]) & 1)) p |= 1 << b;
+  return p;
+}
+__device__ __forceinline__ int pos_lane(const Lay& Y, int lane) {
+  int p = 0;
+#pragma unroll
+  for (int b = 0; b < L; b++)
+    if (Y.s[b] >= 3 && Y.s[b] < 8) p |= ((lane >> Y.s[b]) & 1) << b;
+  return p;
+}
+__device__ __forceinline__ int pos_wave(const Lay& Y, int w) {
+  int p = 0;
+#pragma unroll
+  for (int b = 0; b < L; b++)
+    if (Y.s[b] >= 8) p |= ((w >> (Y.s[b] - 8)) & 1) << b;
+  return p;
+}
+constexpr bool bits_above_in(const Lay& Y, int d, int lo, int hi) {  // any position bit > d in slots [lo, hi)
+  for (int b = d + 1; b < L; b++)
+    if (Y.s[b] >= lo && Y.s[b] < hi) return true;
+  return false;
+}
+
+struct Ctx {
+  const uint16_t* cpoly;  // alpha^skew[i] in the standard basis, 0 = no multiply
+  int plane_lane;         // pos_lane of the current layout is recomputed per layer (cheap, lane-constant)
+  int lane, w;
+};
+
+// One butterfly of layer d (bit d in register slot RB of layout Y) between E[R] and E[R | 1 << RB].
+template <const Lay& Y, bool INVERSE, int D, int R>
+__device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
+  constexpr int RB = Y.s[D];
+  static_assert(RB == 0 || RB == 1, "butterfly bit must sit in a register slot");
+  if constexpr (!((R >> RB) & 1)) {
+    uint32_t(&X)[16] = E[R];
+    uint32_t(&Yv)[16] = E[R | (1 << RB)];
+    constexpr int hi = ~((2 << D) - 1);
+    constexpr int s0r = pos_r(Y, R) & hi;
+    constexpr int base = INVERSE ? (M - 1 + s0r + (1 << D)) : (s0r + (1 << D) - 1);
+    if (INVERSE) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
+    }
+    if constexpr (bits_above_in(Y, D, 3, 8)) {  // per-lane constant
+      const int idx = base + ((pos_lane(Y, cx.lane) + pos_wave(Y, cx.w)) & hi);
+      muladd_lane(X, Yv, cx.cpoly[idx]);
+    } else if constexpr (bits_above_in(Y, D, 8, 16)) {  // wave-uniform constant
+      const int idx = __builtin_amdgcn_readfirstlane(base + (pos_wave(Y, cx.w) & hi));
+      const unsigned c = cx.cpoly[idx];
+      if (c) muladd_uniform(X, Yv, c);
+    } else {  // compile-time constant
+      static_assert(base < kCpoly16N, "constant table too short");
+      muladd_const<kCpoly16[base]>(X, Yv);
+    }
+    if (!INVERSE) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
+    }
+  }
+}
+template <const Lay& Y, bool INVERSE, int D>
+__device__ __forceinline__ void layer(uint32_t (&E)[4][16], const Ctx& cx) {
+  butterfly<Y, INVERSE, D, 0>(E, cx);
+  butterfly<Y, INVERSE, D, 1>(E, cx);
+  butterfly<Y, INVERSE, D, 2>(E, cx);
+  butterfly<Y, INVERSE, D, 3>(E, cx);
+}
+
+// ---- moves between layouts ----------------------------------------------------------------------------------------
+// R0 <-> lane bit 5 and R1 <-> lane bit 4 (LA <-> LB): v_permlane32_swap(a, b) exchanges lanes 32..63 of a with lanes
+// 0..31 of b, i.e. swaps the register bit of the pair (a, b) with lane bit 5; v_permlane16_swap likewise for lane
+// bit 4 (per 32-lane half).  Involution.
+__device__ __forceinline__ void swap_lane45(uint32_t (&E)[4][16]) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    auto p0 = __builtin_amdgcn_permlane32_swap(E[0][j], E[1][j], false, false);
+    E[0][j] = p0[0];
+    E[1][j] = p0[1];
+    auto p1 = __builtin_amdgcn_permlane32_swap(E[2][j], E[3][j], false, false);
+    E[2][j] = p1[0];
+    E[3][j] = p1[1];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    auto p0 = __builtin_amdgcn_permlane16_swap(E[0][j], E[2][j], false, false);
+    E[0][j] = p0[0];
+    E[2][j] = p0[1];
+    auto p1 = __builtin_amdgcn_permlane16_swap(E[1][j], E[3][j], false, false);
+    E[1][j] = p1[0];
+    E[3][j] = p1[1];
+  }
+}
+// R0 <-> lane bit 3 (LB <-> LC): the partner lane (lane ^ 8) via DPP row_ror:8, selects on lm = all-ones in lanes
+// with bit 3 set.  Involution.
+__device__ __forceinline__ uint32_t ror8(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void swap_lane3(uint32_t (&E)[4][16], uint32_t lm) {
+#pragma unroll
+  for (int q = 0; q < 4; q += 2) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t a = E[q][j], b = E[q + 1][j];
+      const uint32_t send = __builtin_amdgcn_bitop3_b32(lm, a, b, 0xCA);  // lm ? a : b
+      const uint32_t recv = ror8(send);
+      E[q][j] = __builtin_amdgcn_bitop3_b32(lm, recv, a, 0xCA);
+      E[q + 1][j] = __builtin_amdgcn_bitop3_b32(lm, b, recv, 0xCA);
+    }
+  }
+}
+// Register bits (R0, R1) <-> wave bits (W_{2H}, W_{2H+1}) through LDS (LC <-> LD: H = 0, LD <-> LE: H = 1).  Slot key
+// (other wave bits, wave pair, register): thread (w, r) writes key (w_other, w_pair, r) and reads key
+// (w_other, r, w_pair); the register equal to the wave pair stays in place.  Two rounds of 8 planes.
+template <int H>
+__device__ __forceinline__ void exchange_w(uint32_t (&E)[4][16], uint4* xb, int w, int lane) {
+  const int wp = (w >> (2 * H)) & 3;
+  const int wo = H == 0 ? (w >> 2) : (w & 3);
+#pragma unroll
+  for (int half = 0; half < 2; half++) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      if (r == wp) continue;
+      uint4* p = xb + ((((wo * 4 + wp) * 4 + r) * 2) * 64 + lane);
+      p[0] = make_uint4(E[r][8 * half + 0], E[r][8 * half + 1], E[r][8 * half + 2], E[r][8 * half + 3]);
+      p[64] = make_uint4(E[r][8 * half + 4], E[r][8 * half + 5], E[r][8 * half + 6], E[r][8 * half + 7]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      if (r == wp) continue;
+      const uint4* p = xb + ((((wo * 4 + r) * 4 + wp) * 2) * 64 + lane);
+      const uint4 v0 = p[0], v1 = p[64];
+      E[r][8 * half + 0] = v0.x;
+      E[r][8 * half + 1] = v0.y;
+      E[r][8 * half + 2] = v0.z;
+      E[r][8 * half + 3] = v0.w;
+      E[r][8 * half + 4] = v1.x;
+      E[r][8 * half + 5] = v1.y;
+      E[r][8 * half + 6] = v1.z;
+      E[r][8 * half + 7] = v1.w;
+    }
+    __syncthreads();
+  }
+}
+
+struct Args {
+  const uint8_t* src;
+  long long src_blk, src_cw, src_sh;
+  uint8_t* dst;
+  long long dst_blk, dst_cw, dst_sh;
+  uint8_t* cpy;
+  long long cpy_blk, cpy_cw, cpy_sh;
+  const uint16_t* cpoly;
+  int cw_per_blk, slices;
+};
+
+__global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int wg = blockIdx.x;
+  const int slice = wg % a.slices;
+  wg /= a.slices;
+  const int cw = wg % a.cw_per_blk, blk = wg / a.cw_per_blk;
+  const int u = lane & 7;
+  const long long off = (long long)slice * 512 + u * 64;
+  const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
+  uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
+  uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
+  Ctx cx{a.cpoly, 0, lane, w};
+  uint32_t lm3 = ((lane >> 3) & 1) ? ~0u : 0u;
+  asm volatile("" : "+v"(lm3));
+
+  uint32_t E[4][16];
+  const SliceMasks km = slice_masks();
+  const int pl = pos_lane(LA, lane) + pos_wave(LA, w);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int s = pl + pos_r(LA, r);  // data shard s sits at point m + s (all k = m shards present)
+    const uint4* p = reinterpret_cast<const uint4*>(src + s * a.src_sh);
+    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    if (cpy) {
+      uint4* o = reinterpret_cast<uint4*>(cpy + s * a.cpy_sh);
+      o[0] = q0;
+      o[1] = q1;
+      o[2] = q2;
+      o[3] = q3;
+    }
+    uint32_t lo[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    uint32_t hi[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    bitslice8(lo, km);
+    bitslice8(hi, km);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      E[r][j] = lo[j];
+      E[r][8 + j] = hi[j];
+    }
+    change_basis<false>(E[r]);
+  }
+  // IFFT, D = 1 .. m/2
+  layer<LA, true, 0>(E, cx);
+  layer<LA, true, 1>(E, cx);
+  swap_lane45(E);
+  layer<LB, true, 2>(E, cx);
+  swap_lane3(E, lm3);
+  layer<LC, true, 3>(E, cx);
+  layer<LC, true, 4>(E, cx);
+  exchange_w<0>(E, xb, w, lane);
+  layer<LD, true, 5>(E, cx);
+  layer<LD, true, 6>(E, cx);
+  exchange_w<1>(E, xb, w, lane);
+  layer<LE, true, 7>(E, cx);
+  layer<LE, true, 8>(E, cx);
+  // FFT, D = m/2 .. 1
+  layer<LE, false, 8>(E, cx);
+  layer<LE, false, 7>(E, cx);
+  exchange_w<1>(E, xb, w, lane);
+  layer<LD, false, 6>(E, cx);
+  layer<LD, false, 5>(E, cx);
+  exchange_w<0>(E, xb, w, lane);
+  layer<LC, false, 4>(E, cx);
+  layer<LC, false, 3>(E, cx);
+  swap_lane3(E, lm3);
+  layer<LB, false, 2>(E, cx);
+  swap_lane45(E);
+  layer<LA, false, 1>(E, cx);
+  layer<LA, false, 0>(E, cx);
+  // parity shard s = point s
+  const SliceMasks ko = slice_masks();
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int s = pl + pos_r(LA, r);
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = E[r][j];
+    change_basis<true>(v);
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      lo[j] = v[j];
+      hi[j] = v[8 + j];
+    }
+    bitslice8(lo, ko);
+    bitslice8(hi, ko);
+    uint4* o = reinterpret_cast<uint4*>(dst + s * a.dst_sh);
+    o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
+    o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+  }
+}
+
+}  // namespace r16
+
+bool rs16_reg_eligible(const RsJob& j) { return j.k == r16::M && j.shard_len % 512 == 0; }
+
+int rs16_reg_init(int device) {
+  (void)device;
+  // the compile-time constants must equal the host-built table (leopard_tables.cpp)
+  const LeoTables& t = leo_tables(16);
+  unsigned st = 1;
+  static uint16_t apow[65535];
+  for (int i = 0; i < 65535; i++) {
+    apow[i] = (uint16_t)st;
+    st <<= 1;
+    if (st & 0x10000) st ^= 0x1002D;
+  }
+  for (int i = 0; i < kCpoly16N; i++) {
+    const uint16_t want = t.skew[i] >= 65535 ? 0 : apow[t.skew[i]];
+    if (want != kCpoly16[i]) return -1;
+  }
+  return hipFuncSetAttribute((const void*)r16::rs_encode16_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             128 * 1024) == hipSuccess
+             ? 0
+             : -1;
+}
+
+int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t s) {
+  if (!rs16_reg_eligible(j)) return -2;
+  r16::Args a;
+  a.src = j.src;
+  a.src_blk = j.src_blk;
+  a.src_cw = j.src_cw;
+  a.src_sh = j.src_sh;
+  a.dst = j.dst;
+  a.dst_blk = j.dst_blk;
+  a.dst_cw = j.dst_cw;
+  a.dst_sh = j.dst_sh;
+  a.cpy = j.cpy;
+  a.cpy_blk = j.cpy_blk;
+  a.cpy_cw = j.cpy_cw;
+  a.cpy_sh = j.cpy_sh;
+  a.cpoly = d_cpoly;
+  a.cw_per_blk = j.cw_per_blk;
+  a.slices = j.shard_len / 512;
+  const long long grid = (long long)j.nblk * j.cw_per_blk * a.slices;
+  if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
+  hipLaunchKernelGGL(r16::rs_encode16_reg_kernel, dim3((unsigned)grid), dim3(1024), 128 * 1024, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cda

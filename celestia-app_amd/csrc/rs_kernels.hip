@@ -834,6 +834,7 @@ int rs16_init_device_tables(int device) {
   if (hipFuncSetAttribute((const void*)rs_encode16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
       hipSuccess)
     return -1;
+  if (rs16_reg_init(device)) return -1;
   g_cpoly16[device] = (uint16_t*)d;
   return 0;
 }
@@ -843,6 +844,13 @@ int launch_rs_encode16(const RsJob& j, hipStream_t s) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 64 || !g_cpoly16[dev]) return -1;
+  // k = 512 codewords of whole 512-B shards: the register-resident encoder (rs16_kernels.hip); CDA_RS16=lds forces
+  // this LDS encoder (same bytes) for A/B runs
+  static const bool force_lds = [] {
+    const char* e = getenv("CDA_RS16");
+    return e && e[0] == 'l';
+  }();
+  if (!force_lds && rs16_reg_eligible(j)) return launch_rs_encode16_reg(j, g_cpoly16[dev], s);
   Rs16Args a;
   a.src = j.src;
   a.src_blk = j.src_blk;
