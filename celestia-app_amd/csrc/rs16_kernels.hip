@@ -28,6 +28,7 @@
 // and one LDS round trip + barrier per layer; here 6 of 18 layers are per-lane and the state crosses LDS 4 times.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "cda_internal.h"
 #include "gf16_const.h"
@@ -186,10 +187,19 @@ constexpr bool bits_above_in(const Lay& Y, int d, int lo, int hi) {  // any posi
   return false;
 }
 
+// The 12 per-lane constants (layers d = 0, 1, 2 of both transforms, two butterflies each) are fetched once at the
+// start, together with the data, two 16-bit values per VGPR: fetched at their layer, each would stall its wave on a
+// global-load round trip inside the compute phase.
+constexpr int lv_slot(bool inv, int d, int r) {  // r = the butterfly's lower register index
+  return (inv ? 0 : 6) + (inv ? d : 2 - d) * 2 + ((r & 1) | (r >> 1));
+}
+// The 16 wave-uniform constants (layers d = 3..6 of both transforms) likewise, into SGPRs.
+constexpr int un_slot(bool inv, int d, int r) { return (inv ? 0 : 8) + (d - 3) * 2 + ((r & 1) | (r >> 1)); }
 struct Ctx {
   const uint16_t* cpoly;  // alpha^skew[i] in the standard basis, 0 = no multiply
-  int plane_lane;         // pos_lane of the current layout is recomputed per layer (cheap, lane-constant)
   int lane, w;
+  uint32_t lv[6];         // packed per-lane constants, slot lv_slot(..)
+  uint32_t un[8];         // packed wave-uniform constants, slot un_slot(..)
 };
 
 // One butterfly of layer d (bit d in register slot RB of layout Y) between E[R] and E[R | 1 << RB].
@@ -207,12 +217,12 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
 #pragma unroll
       for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
     }
-    if constexpr (bits_above_in(Y, D, 3, 8)) {  // per-lane constant
-      const int idx = base + ((pos_lane(Y, cx.lane) + pos_wave(Y, cx.w)) & hi);
-      muladd_lane(X, Yv, cx.cpoly[idx]);
-    } else if constexpr (bits_above_in(Y, D, 8, 16)) {  // wave-uniform constant
-      const int idx = __builtin_amdgcn_readfirstlane(base + (pos_wave(Y, cx.w) & hi));
-      const unsigned c = cx.cpoly[idx];
+    if constexpr (bits_above_in(Y, D, 3, 8)) {  // per-lane constant (preloaded)
+      constexpr int slot = lv_slot(INVERSE, D, R);
+      muladd_lane(X, Yv, (cx.lv[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu);
+    } else if constexpr (bits_above_in(Y, D, 8, 16)) {  // wave-uniform constant (preloaded)
+      constexpr int slot = un_slot(INVERSE, D, R);
+      const unsigned c = (cx.un[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu;
       if (c) muladd_uniform(X, Yv, c);
     } else {  // compile-time constant
       static_assert(base < kCpoly16N, "constant table too short");
@@ -230,6 +240,50 @@ __device__ __forceinline__ void layer(uint32_t (&E)[4][16], const Ctx& cx) {
   butterfly<Y, INVERSE, D, 1>(E, cx);
   butterfly<Y, INVERSE, D, 2>(E, cx);
   butterfly<Y, INVERSE, D, 3>(E, cx);
+}
+
+template <const Lay& Y, bool INVERSE, int D, int R>
+__device__ __forceinline__ void lv_fetch(Ctx& cx) {
+  constexpr int RB = Y.s[D];
+  constexpr int hi = ~((2 << D) - 1);
+  constexpr int base = INVERSE ? (M - 1 + (pos_r(Y, R) & hi) + (1 << D)) : ((pos_r(Y, R) & hi) + (1 << D) - 1);
+  constexpr int slot = lv_slot(INVERSE, D, R);
+  static_assert(!((R >> RB) & 1), "R is the lower register of its butterfly");
+  const uint32_t c = cx.cpoly[base + ((pos_lane(Y, cx.lane) + pos_wave(Y, cx.w)) & hi)];
+  cx.lv[slot >> 1] |= c << (16 * (slot & 1));
+}
+template <const Lay& Y, bool INVERSE, int D, int R>
+__device__ __forceinline__ uint32_t un_fetch(const Ctx& cx) {
+  constexpr int hi = ~((2 << D) - 1);
+  constexpr int base = INVERSE ? (M - 1 + (pos_r(Y, R) & hi) + (1 << D)) : ((pos_r(Y, R) & hi) + (1 << D) - 1);
+  return cx.cpoly[base + (pos_wave(Y, cx.w) & hi)];
+}
+template <bool INVERSE>
+__device__ __forceinline__ void un_fetch_dir(Ctx& cx) {
+  const uint32_t c[8] = {un_fetch<LC, INVERSE, 3, 0>(cx), un_fetch<LC, INVERSE, 3, 1>(cx),
+                         un_fetch<LC, INVERSE, 4, 0>(cx), un_fetch<LC, INVERSE, 4, 2>(cx),
+                         un_fetch<LD, INVERSE, 5, 0>(cx), un_fetch<LD, INVERSE, 5, 2>(cx),
+                         un_fetch<LD, INVERSE, 6, 0>(cx), un_fetch<LD, INVERSE, 6, 1>(cx)};
+  static_assert(un_slot(INVERSE, 6, 1) - un_slot(INVERSE, 3, 0) == 7, "slot order");
+  constexpr int s0 = un_slot(INVERSE, 3, 0) >> 1;
+#pragma unroll
+  for (int i = 0; i < 4; i++) cx.un[s0 + i] = __builtin_amdgcn_readfirstlane(c[2 * i] | (c[2 * i + 1] << 16));
+}
+__device__ __forceinline__ void lv_fetch_all(Ctx& cx) {
+#pragma unroll
+  for (int i = 0; i < 6; i++) cx.lv[i] = 0;
+  lv_fetch<LA, true, 0, 0>(cx);
+  lv_fetch<LA, true, 0, 2>(cx);
+  lv_fetch<LA, true, 1, 0>(cx);
+  lv_fetch<LA, true, 1, 1>(cx);
+  lv_fetch<LB, true, 2, 0>(cx);
+  lv_fetch<LB, true, 2, 2>(cx);
+  lv_fetch<LB, false, 2, 0>(cx);
+  lv_fetch<LB, false, 2, 2>(cx);
+  lv_fetch<LA, false, 1, 0>(cx);
+  lv_fetch<LA, false, 1, 1>(cx);
+  lv_fetch<LA, false, 0, 0>(cx);
+  lv_fetch<LA, false, 0, 2>(cx);
 }
 
 // ---- moves between layouts ----------------------------------------------------------------------------------------
@@ -318,6 +372,7 @@ struct Args {
   long long cpy_blk, cpy_cw, cpy_sh;
   const uint16_t* cpoly;
   int cw_per_blk, slices;
+  int mode;  // diagnostics (CDA_RS16_MODE): 0 = encode; 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores
 };
 
 __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
@@ -333,7 +388,10 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
   uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
   uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
-  Ctx cx{a.cpoly, 0, lane, w};
+  Ctx cx{a.cpoly, lane, w, {}, {}};
+  lv_fetch_all(cx);
+  un_fetch_dir<true>(cx);
+  un_fetch_dir<false>(cx);
   uint32_t lm3 = ((lane >> 3) & 1) ? ~0u : 0u;
   asm volatile("" : "+v"(lm3));
 
@@ -344,7 +402,12 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   for (int r = 0; r < 4; r++) {
     const int s = pl + pos_r(LA, r);  // data shard s sits at point m + s (all k = m shards present)
     const uint4* p = reinterpret_cast<const uint4*>(src + s * a.src_sh);
-    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    uint4 q0, q1, q2, q3;
+    if (a.mode < 2) {  // modes >= 2: synthetic data, no loads
+      q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    } else {
+      q0 = make_uint4(s, lane, w, r), q1 = make_uint4(lane * 3, s ^ 5, 7, w), q2 = q0, q3 = q1;
+    }
     if (cpy) {
       uint4* o = reinterpret_cast<uint4*>(cpy + s * a.cpy_sh);
       o[0] = q0;
@@ -363,6 +426,7 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
     }
     change_basis<false>(E[r]);
   }
+  if (a.mode == 1) goto store;
   // IFFT, D = 1 .. m/2
   layer<LA, true, 0>(E, cx);
   layer<LA, true, 1>(E, cx);
@@ -391,6 +455,8 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   swap_lane45(E);
   layer<LA, false, 1>(E, cx);
   layer<LA, false, 0>(E, cx);
+store:
+  if (a.mode == 3 && blockIdx.x != 0x7FFFFFFF) return;
   // parity shard s = point s
   const SliceMasks ko = slice_masks();
 #pragma unroll
@@ -459,6 +525,11 @@ int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t 
   a.cpoly = d_cpoly;
   a.cw_per_blk = j.cw_per_blk;
   a.slices = j.shard_len / 512;
+  static const int mode = [] {
+    const char* e = getenv("CDA_RS16_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  a.mode = mode;
   const long long grid = (long long)j.nblk * j.cw_per_blk * a.slices;
   if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
   hipLaunchKernelGGL(r16::rs_encode16_reg_kernel, dim3((unsigned)grid), dim3(1024), 128 * 1024, s, a);
