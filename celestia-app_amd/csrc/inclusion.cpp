@@ -18,36 +18,11 @@
 #include <vector>
 
 #include "ctx.h"
+#include "plan.h"
 
 using namespace cda;
 
 namespace {
-
-constexpr uint32_t kFirstSparse = CDA_SHARE - CDA_NAMESPACE_SIZE - 1 - 4;  // 478 (specs shares.md:31-60)
-constexpr uint32_t kContSparse = CDA_SHARE - CDA_NAMESPACE_SIZE - 1;       // 482
-
-uint32_t sparse_shares_needed(uint64_t len) {  // shares.SparseSharesNeeded
-  if (len == 0) return 0;
-  if (len <= kFirstSparse) return 1;
-  return 1 + (uint32_t)((len - kFirstSparse + kContSparse - 1) / kContSparse);
-}
-uint32_t round_up_pow2(uint32_t v) {
-  uint32_t p = 1;
-  while (p < v) p <<= 1;
-  return p;
-}
-uint32_t round_down_pow2(uint32_t v) {
-  uint32_t p = 1;
-  while (p * 2 <= v) p <<= 1;
-  return p;
-}
-// inclusion.SubTreeWidth: min(RoundUpPowerOfTwo(ceil(n / threshold)), BlobMinSquareSize(n))
-uint32_t subtree_width(uint32_t n, uint32_t threshold) {
-  const uint32_t s = round_up_pow2(n / threshold + (n % threshold ? 1 : 0));
-  uint32_t r = 0;
-  while ((uint64_t)r * r < n) r++;
-  return std::min(s, round_up_pow2(r));
-}
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
@@ -62,28 +37,11 @@ int square_k(uint32_t count, uint32_t share_len, uint32_t* k, cda_err_info* err)
   return CDA_OK;
 }
 
-// A perfect tree of w leaves exported as levels (leaves first, root last), 90 B per node.
-struct TreeView {
-  const uint8_t* base;
-  uint32_t w;
-  const uint8_t* node(int h, uint32_t p) const {
-    size_t off = 0;
-    for (int i = 0; i < h; i++) off += w >> i;
-    return base + (off + p) * CDA_NODE_SIZE;
-  }
-};
-
-// nmt buildRangeProof (ProveRange, called at pkg/proof/proof.go:142) on a perfect tree:
-// the maximal subtrees outside [s, e), left to right.
-void prove_rec(const TreeView& t, int h, uint32_t p, uint32_t s, uint32_t e, std::vector<const uint8_t*>& out) {
-  const uint32_t lo = p << h, hi = (p + 1) << h;
-  if (hi <= s || lo >= e) {
-    out.push_back(t.node(h, p));
-    return;
-  }
-  if (h == 0) return;  // a leaf inside the range
-  prove_rec(t, h - 1, 2 * p, s, e, out);
-  prove_rec(t, h - 1, 2 * p + 1, s, e, out);
+// node (h, p) of a perfect tree of w leaves exported as levels (leaves first, root last), 90 B per node
+const uint8_t* tree_node(const uint8_t* base, uint32_t w, int h, uint32_t p) {
+  size_t off = 0;
+  for (int i = 0; i < h; i++) off += w >> i;
+  return base + (off + p) * CDA_NODE_SIZE;
 }
 
 }  // namespace
@@ -115,17 +73,12 @@ int cda_blob_commitments(cda_ctx* c, uint32_t nblobs, const uint8_t* namespaces,
     d.data_off = offsets[b] - offsets[0];
     d.len = (uint32_t)len;
     d.share_off = (uint32_t)total;
-    d.nshares = sparse_shares_needed(len);
-    d.width = subtree_width(d.nshares, subtree_root_threshold);
+    d.nshares = plan::sparse_shares_needed(len);
+    d.width = plan::subtree_width(d.nshares, subtree_root_threshold);
     memcpy(d.ns, namespaces + (size_t)b * CDA_NAMESPACE_SIZE, CDA_NAMESPACE_SIZE);
     d.ns[CDA_NAMESPACE_SIZE] = (uint8_t)ver;
     set_off[b] = (uint32_t)tree_rec.size();
-    for (uint32_t j = 0, rem = d.nshares; rem;) {  // MerkleMountainRangeSizes: first share of each mountain
-      const uint32_t t = rem >= d.width ? d.width : round_down_pow2(rem);
-      tree_rec.push_back((uint32_t)total + j);
-      j += t;
-      rem -= t;
-    }
+    plan::mountains(d.nshares, d.width, (uint32_t)total, tree_rec);  // first share of each mountain
     max_trees = std::max<uint32_t>(max_trees, (uint32_t)tree_rec.size() - set_off[b]);
     max_w = std::max(max_w, d.width);
     total += d.nshares;
@@ -370,13 +323,15 @@ int cda_share_inclusion_proof(cda_ctx* c, uint32_t count, uint32_t share_len, co
     }
     // NMT range proof inside the row: [startLeaf, k) on the first row, [0, k) between, [0, endLeaf] on the last
     const uint32_t s = i == 0 ? start % k : 0, e = i + 1 == info->nrows ? (end - 1) % k + 1 : k;
-    std::vector<const uint8_t*> nodes;
-    prove_rec(TreeView{rn.data() + (size_t)r * per_tree * CDA_NODE_SIZE, w}, L, 0, s, e, nodes);
+    std::vector<std::pair<int, uint32_t>> nodes;
+    plan::prove_range(L, s, e, nodes);
     nmt_start[i] = (int32_t)s;
     nmt_end[i] = (int32_t)e;
     nmt_count[i] = (int32_t)nodes.size();
+    const uint8_t* tree = rn.data() + (size_t)r * per_tree * CDA_NODE_SIZE;
     for (size_t q = 0; q < nodes.size(); q++)
-      memcpy(nmt_nodes + ((size_t)i * info->max_nodes + q) * CDA_NODE_SIZE, nodes[q], CDA_NODE_SIZE);
+      memcpy(nmt_nodes + ((size_t)i * info->max_nodes + q) * CDA_NODE_SIZE,
+             tree_node(tree, w, nodes[q].first, nodes[q].second), CDA_NODE_SIZE);
   }
   if (data_root) memcpy(data_root, root, 32);
   return CDA_OK;

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "plan.h"
 
 using namespace cda;
 
@@ -42,74 +43,8 @@ static int ensure_host(cda_ctx* c, cda_ctx::Buf& b, size_t bytes) {
 // first batch with a failing root check is replayed one operation at a time
 // (see below), so a Byzantine report and the square left "most repaired prior
 // to the Byzantine axis" are exactly the sequential reference's.
-namespace {
-inline int enc_axis(int axis, int idx) { return (axis << 24) | idx; }
-
-// Presence of the w x w cells as row and column bitsets with per-axis counts: a crossword step
-// costs O(w / 64 + cells it fills) on the host instead of O(w) byte scans.
-struct Presence {
-  int w = 0, words = 0;
-  uint64_t full = 0;              // valid bits of each word (w < 64: one partial word)
-  std::vector<uint64_t> bits[2];  // [axis][idx * words + j / 64] bit j % 64 = cell j of axis idx present
-  std::vector<int> cnt[2];        // present cells per axis
-  void init(int w_, const uint8_t* p) {
-    w = w_;
-    words = (w + 63) / 64;
-    full = w >= 64 ? ~0ull : ((1ull << w) - 1);
-    for (int a = 0; a < 2; a++) {
-      bits[a].assign((size_t)w * words, 0);
-      cnt[a].assign(w, 0);
-    }
-    for (int r = 0; r < w; r++)
-      for (int q = 0; q < w; q++)
-        if (p[(size_t)r * w + q]) {
-          bits[CDA_AXIS_ROW][(size_t)r * words + (q >> 6)] |= 1ull << (q & 63);
-          bits[CDA_AXIS_COL][(size_t)q * words + (r >> 6)] |= 1ull << (r & 63);
-          cnt[CDA_AXIS_ROW][r]++;
-          cnt[CDA_AXIS_COL][q]++;
-        }
-  }
-  // f(j) for every missing cell j of axis (a, idx), j ascending
-  template <class F>
-  void missing(int a, int idx, F f) const {
-    const uint64_t* b = bits[a].data() + (size_t)idx * words;
-    for (int wd = 0; wd < words; wd++)
-      for (uint64_t m = ~b[wd] & full; m; m &= m - 1) f(wd * 64 + __builtin_ctzll(m));
-  }
-  // mark every cell of axis (a, idx) present
-  void fill(int a, int idx) {
-    const int o = 1 - a;
-    missing(a, idx, [&](int j) {
-      bits[o][(size_t)j * words + (idx >> 6)] |= 1ull << (idx & 63);
-      cnt[o][j]++;
-    });
-    uint64_t* b = bits[a].data() + (size_t)idx * words;
-    for (int wd = 0; wd < words; wd++) b[wd] = full;
-    cnt[a][idx] = w;
-  }
-  // presence of axis (a, idx)'s cells, one byte (0/1) each
-  void bytes(int a, int idx, uint8_t* out) const {
-    static const struct Expand {
-      uint64_t t[256];
-      Expand() {
-        for (int v = 0; v < 256; v++) {
-          t[v] = 0;
-          for (int i = 0; i < 8; i++) t[v] |= (uint64_t)((v >> i) & 1) << (8 * i);
-        }
-      }
-    } ex;
-    const uint64_t* b = bits[a].data() + (size_t)idx * words;
-    if (w < 8) {
-      for (int j = 0; j < w; j++) out[j] = (b[0] >> j) & 1;
-      return;
-    }
-    for (int j = 0; j < w; j += 8) {
-      const uint64_t v = ex.t[(b[j >> 6] >> (j & 63)) & 0xFF];
-      memcpy(out + j, &v, 8);
-    }
-  }
-};
-}  // namespace
+using plan::enc_axis;
+using plan::Presence;
 
 // Repair of the square in host memory `eds` (uploaded, repaired, copied back) or, when eds is null,
 // of the square already in device memory d_eds_in; the caller holds the lock for stream s.
@@ -199,92 +134,22 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   P.init(w, present);
   const uint8_t* want[2] = {row_roots, col_roots};
 
-  // ---- plan: prerepairSanityCheck axes, then every crossword sweep on the optimistic presence ----
-  std::vector<int> sane;  // complete axes: i ascending, row before column
-  for (int i = 0; i < w; i++) {
-    if (P.cnt[CDA_AXIS_ROW][i] == w) sane.push_back(enc_axis(CDA_AXIS_ROW, i));
-    if (P.cnt[CDA_AXIS_COL][i] == w) sane.push_back(enc_axis(CDA_AXIS_COL, i));
+  // ---- plan: prerepairSanityCheck axes, then every crossword sweep on the optimistic presence (plan.cpp) ----
+  plan::RepairPlan rp;
+  if ((rc = plan::plan_repair(P, K, rp, h + o_pres))) return rc;
+  const std::vector<int>& sane = rp.sane;
+  const std::vector<plan::RepairOp>& ops = rp.ops;
+  const std::vector<plan::RepairBatch>& bat = rp.bat;
+  const std::vector<int>& vall = rp.vall;
+  const std::vector<int>& blast = rp.blast;  // rows go back to the caller once their last writer has run
+  const bool solved = rp.solved;
+  for (size_t q = 0; q < ops.size(); q++) {
+    const plan::RepairOp& op = ops[q];
+    ((long long*)(h + o_off))[q] =
+        op.axis == CDA_AXIS_ROW ? (long long)op.idx * w * CDA_SHARE : (long long)op.idx * CDA_SHARE;
+    ((long long*)(h + o_str))[q] = op.axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
   }
-  struct Op {
-    int axis, idx;
-    std::vector<int> ortho;
-  };
-  struct Batch {
-    size_t q0, q1, v0, v1;  // operations [q0, q1), their verified axes vall[v0, v1)
-  };
-  std::vector<Op> ops;
-  std::vector<Batch> bat;
-  std::vector<int> vall;
-  bool solved = false;
-  {
-    Presence Pq = P;
-    for (;;) {
-      // replay one sweep: row i, then column i, for i = 0..w-1
-      Presence Ps = Pq;
-      const size_t first = ops.size();
-      bool sweep_solved = true;
-      for (int i = 0; i < w; i++) {
-        for (int axis = 0; axis < 2; axis++) {
-          const int n = Ps.cnt[axis][i];
-          if (n == w) continue;
-          if (n < K) {
-            sweep_solved = false;
-            continue;
-          }
-          Op op{axis, i, {}};
-          const int oaxis = 1 - axis;
-          // orthogonal axis j is completed by this operation iff (i, j) is its only missing cell
-          Ps.missing(axis, i, [&](int j) {
-            if (Ps.cnt[oaxis][j] == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
-          });
-          Ps.fill(axis, i);
-          ops.push_back(std::move(op));
-        }
-      }
-      if (ops.size() > 2 * W) return CDA_E_ARG;  // cannot happen: each operation completes an axis
-      // batches of operations already decodable at the batch start
-      for (size_t b0 = first; b0 < ops.size();) {
-        size_t b1 = b0;
-        while (b1 < ops.size() && Pq.cnt[ops[b1].axis][ops[b1].idx] >= K) b1++;
-        if (b1 == b0) return CDA_E_ARG;  // cannot happen: the replay guarantees decodability in order
-        Batch bt{b0, b1, vall.size(), 0};
-        for (size_t q = b0; q < b1; q++) {
-          const Op& op = ops[q];
-          ((long long*)(h + o_off))[q] =
-              op.axis == CDA_AXIS_ROW ? (long long)op.idx * w * CDA_SHARE : (long long)op.idx * CDA_SHARE;
-          ((long long*)(h + o_str))[q] = op.axis == CDA_AXIS_ROW ? CDA_SHARE : (long long)w * CDA_SHARE;
-          Pq.bytes(op.axis, op.idx, h + o_pres + q * W);  // the presence at the batch start
-          vall.push_back(enc_axis(op.axis, op.idx));      // own axis, then orthogonal axes, in order
-          for (int o : op.ortho) vall.push_back(o);
-        }
-        bt.v1 = vall.size();
-        bat.push_back(bt);
-        for (size_t q = b0; q < b1; q++) Pq.fill(ops[q].axis, ops[q].idx);
-        b0 = b1;
-      }
-      if (sweep_solved) {
-        solved = true;
-        break;
-      }
-      if (ops.size() == first) break;  // no progress: unrepairable once every batch has passed
-    }
-  }
-  if (vall.size() > 4 * W) return CDA_E_ARG;  // cannot happen: the bound above
   const size_t nbat = bat.size();
-  // Host buffers: rows go back to the caller while later batches still run.  blast[r] = the last batch that writes
-  // a cell of row r (a row operation on r, or a column operation with (r, c) missing at its batch start); once that
-  // batch's decode has finished the row holds its final bytes if every check passes.
-  std::vector<int> blast(w, -1);
-  for (size_t b = 0; b < nbat; b++)
-    for (size_t q = bat[b].q0; q < bat[b].q1; q++) {
-      if (ops[q].axis == CDA_AXIS_ROW) {
-        blast[ops[q].idx] = (int)b;
-        continue;
-      }
-      const uint8_t* pr = h + o_pres + q * W;
-      for (int j = 0; j < w; j++)
-        if (!pr[j]) blast[j] = (int)b;
-    }
   const bool early = eds && !c->prof && nbat > 0 && c->repair_early;
   std::vector<hipEvent_t> bev(early ? nbat : 0, nullptr);
   struct EventsGuard {
@@ -445,7 +310,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   // exactly the sequential ones even when a row and a column of a batch write the same cell.
   auto enqueue_batches = [&](size_t from) -> int {
     for (size_t b = from; b < nbat; b++) {
-      const Batch& bt = bat[b];
+      const plan::RepairBatch& bt = bat[b];
       {
         ProfScope ps(c, "repair_decode", s);
         const int lr = launch_rs_decode(d_eds, (const long long*)(dd + o_off) + bt.q0,

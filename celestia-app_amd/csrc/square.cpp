@@ -7,39 +7,10 @@
 #include <vector>
 
 #include "ctx.h"
+#include "plan.h"
 
 using namespace cda;
 
-namespace {
-
-// shares a sequence of `len` bytes needs (compact: 474 / 478 per share; sparse: 478 / 482)
-uint64_t shares_needed(uint32_t kind, uint64_t len) {
-  if (kind == CDA_SEG_PADDING || len == 0) return kind == CDA_SEG_PADDING ? 1 : 0;
-  const uint64_t first = kind == CDA_SEG_COMPACT ? 474 : 478, cont = kind == CDA_SEG_COMPACT ? 478 : 482;
-  return len <= first ? 1 : 1 + (len - first + cont - 1) / cont;
-}
-
-// The plan must tile [0, k*k) in order, keep every payload inside `data` and fit its sequence.
-int check_plan(uint32_t k, uint32_t nseg, const cda_share_segment* segs, uint64_t data_len, uint32_t nreserved) {
-  if (!segs || nseg == 0) return CDA_E_ARG;
-  uint64_t next = 0;
-  for (uint32_t i = 0; i < nseg; i++) {
-    const cda_share_segment& s = segs[i];
-    if (s.kind > CDA_SEG_PADDING || s.first_share != next || s.nshares == 0) return CDA_E_ARG;
-    if (s.share_version != 0) return CDA_E_SHARE_VERSION;  // appconsts.SupportedShareVersions = {0}
-    if (s.kind != CDA_SEG_PADDING) {
-      if (s.data_off > data_len || s.data_len > data_len - s.data_off || s.data_len > 0xFFFFFFFFull) return CDA_E_ARG;
-      if (shares_needed(s.kind, s.data_len) != s.nshares) return CDA_E_ARG;
-    } else if (s.data_len != 0) {
-      return CDA_E_ARG;
-    }
-    if (s.kind == CDA_SEG_COMPACT && ((uint64_t)s.reserved_off + s.nshares > nreserved)) return CDA_E_ARG;
-    next += s.nshares;
-  }
-  return next == (uint64_t)k * k ? CDA_OK : CDA_E_ARG;
-}
-
-}  // namespace
 
 extern "C" {
 
@@ -47,7 +18,7 @@ int cda_build_ods_device(cda_ctx* c, uint32_t k, uint32_t nseg, const cda_share_
                          uint64_t data_len, const uint32_t* reserved, uint32_t nreserved, void* d_ods, void* stream) {
   CDA_API_TRY
   if (!c || !d_ods || !is_pow2(k) || k > kMaxDeviceK) return CDA_E_ARG;
-  if (int rc = check_plan(k, nseg, segs, data_len, nreserved)) return rc;
+  if (int rc = plan::check_square_plan(k, nseg, segs, data_len, nreserved)) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : nullptr;
   DevLock l(c, s);
   const size_t seg_b = (size_t)nseg * sizeof(cda_share_segment), res_b = (size_t)nreserved * 4;

@@ -26,7 +26,8 @@ E_SHARE_VERSION, E_BLOB_SIZE = -13, -14
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(ORACLE_DIR, "liboracle.so")
+        # CDA_ORACLE_LIB: another build of the same sources (scripts/sanitize.sh: the ASan/UBSan one)
+        path = os.environ.get("CDA_ORACLE_LIB") or os.path.join(ORACLE_DIR, "liboracle.so")
         if not os.path.exists(path):
             subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
         L = ctypes.CDLL(path)
