@@ -21,6 +21,7 @@ import (
 	"github.com/stretchr/testify/require"
 
 	"github.com/celestiaorg/celestia-app/v2/pkg/cda"
+	"github.com/celestiaorg/celestia-app/v2/pkg/da"
 	"github.com/celestiaorg/celestia-app/v2/pkg/wrapper"
 )
 
@@ -127,6 +128,28 @@ func TestExtendSharesMatchesCPUPath(t *testing.T) {
 		gc, _ := got.ColRoots()
 		require.Equal(t, wr, gr, "k=%d", k)
 		require.Equal(t, wc, gc, "k=%d", k)
+	}
+}
+
+func TestExtendSquareSplitMatchesCPUPath(t *testing.T) {
+	m, err := cda.NewMulti(0)
+	require.NoError(t, err)
+	defer m.Close()
+	r := rand.New(rand.NewSource(5))
+	for _, k := range []int{1, 4, 32, 128} {
+		s := sortedShares(r, k*k)
+		want, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+		require.NoError(t, err)
+		got, err := m.ExtendSquareSplit(s, true)
+		require.NoError(t, err)
+		require.Equal(t, want.Flattened(), got.EDS.Flattened(), "k=%d", k)
+		wr, _ := want.RowRoots()
+		wc, _ := want.ColRoots()
+		require.Equal(t, wr, got.RowRoots, "k=%d", k)
+		require.Equal(t, wc, got.ColRoots, "k=%d", k)
+		dah, err := da.NewDataAvailabilityHeader(want)
+		require.NoError(t, err)
+		require.Equal(t, dah.Hash(), got.DataHash, "k=%d", k)
 	}
 }
 

@@ -175,3 +175,49 @@ func (m *Multi) ExtendBlocks(blocks [][][]byte, withEDS bool) ([]Block, error) {
 	}
 	return out, nil
 }
+
+// ExtendSquareSplit extends and commits ONE square with its work split over the handle's devices
+// (cda_multi_extend_commit_split, SURVEY.md §8e config C5): the row pass, the exchange of row-encoded shares and
+// leaf records over RCCL, the column pass and the tree folds run on every device, the DAH on the first.  The
+// result equals ExtendShares on the same shares; with withEDS false only the roots and the data hash come back.
+func (m *Multi) ExtendSquareSplit(s [][]byte, withEDS bool) (Block, error) {
+	count := len(s)
+	if !isPowerOfTwo(count) {
+		return Block{}, fmt.Errorf("number of shares is not a power of 2: got %d", count)
+	}
+	k := squareSize(count)
+	if k*k != count {
+		return Block{}, &Error{Code: ErrCodeNotSquare, Axis: -1, Index: -1, Leaf: -1, Block: 0}
+	}
+	flat, n, err := flatten(s)
+	if err != nil {
+		return Block{}, err
+	}
+	if n != ShareSize {
+		return Block{}, fmt.Errorf("shares are %d bytes, the split path takes %d", n, ShareSize)
+	}
+	w := 2 * k
+	var eds []byte
+	if withEDS {
+		eds = make([]byte, w*w*ShareSize)
+	}
+	rows := make([]byte, w*NodeSize)
+	cols := make([]byte, w*NodeSize)
+	dah := make([]byte, 32)
+	var info C.cda_err_info
+	rc := C.cda_multi_extend_commit_split(m.m, C.uint32_t(k), ptr(flat), ptr(eds), ptr(rows), ptr(cols), ptr(dah), &info)
+	if rc != 0 {
+		return Block{}, toErr(rc, &info)
+	}
+	out := Block{RowRoots: split(rows, w), ColRoots: split(cols, w), DataHash: dah}
+	if withEDS {
+		ctx, err := DefaultOn(int(C.cda_multi_device(m.m, 0)))
+		if err != nil {
+			return Block{}, err
+		}
+		if out.EDS, err = importWithRoots(ctx, eds, w, ShareSize, rows, cols); err != nil {
+			return Block{}, err
+		}
+	}
+	return out, nil
+}

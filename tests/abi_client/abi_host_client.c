@@ -144,6 +144,14 @@ int main(int argc, char** argv) {
     fprintf(stderr, "multi-device DAH differs\n");
     return 1;
   }
+  /* one square split over the same devices (C5): same roots and DAH as the single-device call */
+  rc = cda_multi_extend_commit_split(multi, k, ods, NULL, rows3, cols3, dahm, &err);
+  if (rc) return fail("cda_multi_extend_commit_split", rc, &err);
+  if (memcmp(dahm, dah, 32) != 0 || memcmp(rows3, rows, (size_t)w * CDA_NODE_SIZE) != 0 ||
+      memcmp(cols3, cols, (size_t)w * CDA_NODE_SIZE) != 0) {
+    fprintf(stderr, "split DAH / roots differ\n");
+    return 1;
+  }
   cda_multi_free(multi);
 
   if (write_file(argv[3], "commitments.bin", commitments, sizeof commitments) ||
