@@ -17,6 +17,10 @@ struct Stager;  // staging.cpp
 
 struct cda_ctx {
   int device = 0;
+  // the CPUs of the GPU's NUMA node that this process may run on (sysfs local_cpulist of its PCI function
+  // intersected with the affinity at cda_init); libcda's copy helper threads run there, so the pinned staging
+  // rings they allocate and fill sit next to the GPU.  Empty: no binding (CDA_NUMA_BIND=0, or unknown).
+  std::vector<int> local_cpus;
   std::recursive_mutex mu;
   hipStream_t stream = nullptr;
   // CDA_REPAIR_OVERLAP=0: repair verifies each batch on the decode stream instead of a second stream
@@ -54,6 +58,8 @@ struct cda_ctx {
   hipEvent_t sp_ev[2] = {};  // replicas transport: sender-side "ready" events
   // repair: device root table + per-sweep descriptors, and their pinned host staging
   Buf rdesc, rstage;
+  // repair: the present cells of a sparse caller square packed (upload) and their run table
+  Buf rcompact, rruns;
   // pinned staging rings for cda_repair's large copies of caller (pageable) memory, one per direction
   // (staging.cpp); CDA_STAGING: bit 0 stages uploads, bit 1 downloads (0 = plain hipMemcpyAsync)
   cda::Stager* st_in = nullptr;
@@ -100,6 +106,15 @@ void free_pipeline(cda_ctx* c);
 int staged_h2d(cda_ctx* c, void* d_dst, const void* h_src, size_t n, hipStream_t s);
 int staged_d2h(cda_ctx* c, void* h_dst, const void* d_src, size_t n, hipStream_t s);
 void free_staging(cda_ctx* c);
+// byte range [off, off + len) of a host buffer
+struct HostRun {
+  size_t off, len;
+};
+// the runs of h_base, concatenated, to d_dst (through the pinned ring; no pinned fast path)
+int staged_h2d_runs(cda_ctx* c, void* d_dst, const uint8_t* h_base, const HostRun* runs, size_t nruns,
+                    hipStream_t s);
+void bind_helper_thread(const cda_ctx* c);  // the calling helper thread -> c->local_cpus (no-op if empty)
+void find_local_cpus(cda_ctx* c);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 // split_kernels.hip

@@ -290,6 +290,7 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
   if (const char* e = getenv("CDA_STAGING")) c->staging = atoi(e) & 3;
+  find_local_cpus(c);
   // the streams that overlap each other, created right after `stream` so that they land on distinct hardware
   // queues (HIP assigns streams to its GPU_MAX_HW_QUEUES = 4 queues round-robin)
   bool ok = ensure_pipeline(c) == CDA_OK &&
@@ -313,7 +314,7 @@ void cda_free(cda_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     flush_profile(c);
     for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status, &c->plan, &c->payload,
-                    &c->rdesc, &c->sp_ods, &c->sp_R, &c->sp_LR, &c->sp_S, &c->sp_C, &c->sp_LC, &c->sp_scratch,
+                    &c->rdesc, &c->rcompact, &c->rruns, &c->sp_ods, &c->sp_R, &c->sp_LR, &c->sp_S, &c->sp_C, &c->sp_LC, &c->sp_scratch,
                     &c->sp_meta, &c->sp_gather})
       if (b->p) (void)hipFree(b->p);
     for (auto e : c->sp_ev)

@@ -8,6 +8,26 @@
 namespace cda {
 namespace plan {
 
+namespace {
+// 8 presence bytes (any nonzero = present) -> 8 bits, byte i -> bit i
+inline uint64_t pack8(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  v = (((v & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | v) & 0x8080808080808080ull;
+  return ((v >> 7) * 0x0102040810204080ull) >> 56;
+}
+// in place: a[i] bit j <-> a[j] bit i
+void transpose64(uint64_t a[64]) {
+  uint64_t m = 0x00000000FFFFFFFFull;
+  for (int j = 32; j; j >>= 1, m ^= m << j)
+    for (int k = 0; k < 64; k = ((k | j) + 1) & ~j) {
+      const uint64_t t = ((a[k] >> j) ^ a[k | j]) & m;
+      a[k] ^= t << j;
+      a[k | j] ^= t;
+    }
+}
+}  // namespace
+
 void Presence::init(int w_, const uint8_t* p) {
   w = w_;
   words = (w + 63) / 64;
@@ -16,25 +36,31 @@ void Presence::init(int w_, const uint8_t* p) {
     bits[a].assign((size_t)w * words, 0);
     cnt[a].assign(w, 0);
   }
-  for (int r = 0; r < w; r++)
-    for (int q = 0; q < w; q++)
-      if (p[(size_t)r * w + q]) {
-        bits[CDA_AXIS_ROW][(size_t)r * words + (q >> 6)] |= 1ull << (q & 63);
-        bits[CDA_AXIS_COL][(size_t)q * words + (r >> 6)] |= 1ull << (r & 63);
-        cnt[CDA_AXIS_ROW][r]++;
-        cnt[CDA_AXIS_COL][q]++;
-      }
-}
-
-void Presence::fill(int a, int idx) {
-  const int o = 1 - a;
-  missing(a, idx, [&](int j) {
-    bits[o][(size_t)j * words + (idx >> 6)] |= 1ull << (idx & 63);
-    cnt[o][j]++;
-  });
-  uint64_t* b = bits[a].data() + (size_t)idx * words;
-  for (int wd = 0; wd < words; wd++) b[wd] = full;
-  cnt[a][idx] = w;
+  uint64_t* rb = bits[CDA_AXIS_ROW].data();
+  for (int r = 0; r < w; r++) {
+    const uint8_t* row = p + (size_t)r * w;
+    if (w < 8) {
+      for (int q = 0; q < w; q++) rb[(size_t)r * words] |= (uint64_t)(row[q] != 0) << q;
+    } else {
+      for (int q = 0; q < w; q += 8) rb[(size_t)r * words + (q >> 6)] |= pack8(row + q) << (q & 63);
+    }
+    int n = 0;
+    for (int wd = 0; wd < words; wd++) n += __builtin_popcountll(rb[(size_t)r * words + wd]);
+    cnt[CDA_AXIS_ROW][r] = n;
+  }
+  // column bitsets: 64 x 64 bit-block transposes of the row bitsets
+  uint64_t blk[64];
+  for (int R = 0; R < words; R++)
+    for (int C = 0; C < words; C++) {
+      for (int i = 0; i < 64; i++) blk[i] = R * 64 + i < w ? rb[(size_t)(R * 64 + i) * words + C] : 0;
+      transpose64(blk);
+      for (int j = 0; j < 64 && C * 64 + j < w; j++) bits[CDA_AXIS_COL][(size_t)(C * 64 + j) * words + R] = blk[j];
+    }
+  for (int q = 0; q < w; q++) {
+    int n = 0;
+    for (int wd = 0; wd < words; wd++) n += __builtin_popcountll(bits[CDA_AXIS_COL][(size_t)q * words + wd]);
+    cnt[CDA_AXIS_COL][q] = n;
+  }
 }
 
 void Presence::bytes(int a, int idx, uint8_t* out) const {
@@ -67,6 +93,9 @@ int plan_repair(const Presence& P, int K, RepairPlan& out, uint8_t* pres_out) {
     if (P.cnt[CDA_AXIS_COL][i] == w) out.sane.push_back(enc_axis(CDA_AXIS_COL, i));
   }
   std::vector<RepairOp>& ops = out.ops;
+  ops.reserve(2 * W);
+  out.vall.reserve(4 * W);
+  out.blast.assign(w, -1);
   Presence Pq = P;  // the optimistic presence at the start of the next batch
   for (;;) {
     // replay one sweep: row i, then column i, for i = 0..w-1
@@ -81,14 +110,11 @@ int plan_repair(const Presence& P, int K, RepairPlan& out, uint8_t* pres_out) {
           sweep_solved = false;
           continue;
         }
-        RepairOp op{axis, i, {}};
-        const int oaxis = 1 - axis;
+        ops.push_back(RepairOp{axis, i, {}});
         // orthogonal axis j is completed by this operation iff (i, j) is its only missing cell
-        Ps.missing(axis, i, [&](int j) {
-          if (Ps.cnt[oaxis][j] == w - 1) op.ortho.push_back(enc_axis(oaxis, j));
+        Ps.fill(axis, i, [&](int o, int j, int n) {
+          if (n == w) ops.back().ortho.push_back(enc_axis(o, j));
         });
-        Ps.fill(axis, i);
-        ops.push_back(std::move(op));
       }
     }
     if (ops.size() > 2 * W) return CDA_E_ARG;  // cannot happen: each operation completes an axis
@@ -103,10 +129,16 @@ int plan_repair(const Presence& P, int K, RepairPlan& out, uint8_t* pres_out) {
         Pq.bytes(op.axis, op.idx, pres_out + q * W);  // the presence at the batch start
         out.vall.push_back(enc_axis(op.axis, op.idx));
         for (int o : op.ortho) out.vall.push_back(o);
+        // blast[r] = the last batch that writes a cell of row r (a row operation on r, or a column operation
+        // with (r, c) missing at its batch start)
+        if (op.axis == CDA_AXIS_ROW)
+          out.blast[op.idx] = (int)out.bat.size();
+        else
+          Pq.missing(CDA_AXIS_COL, op.idx, [&](int r) { out.blast[r] = (int)out.bat.size(); });
       }
       bt.v1 = out.vall.size();
       out.bat.push_back(bt);
-      for (size_t q = b0; q < b1; q++) Pq.fill(ops[q].axis, ops[q].idx);
+      for (size_t q = b0; q < b1; q++) Pq.fill(ops[q].axis, ops[q].idx, [](int, int, int) {});
       b0 = b1;
     }
     if (sweep_solved) {
@@ -116,19 +148,6 @@ int plan_repair(const Presence& P, int K, RepairPlan& out, uint8_t* pres_out) {
     if (ops.size() == first) break;  // no progress: unrepairable once every batch has passed
   }
   if (out.vall.size() > 4 * W) return CDA_E_ARG;  // each axis is verified by its own and at most one other op
-  // blast[r] = the last batch that writes a cell of row r (a row operation on r, or a column operation with
-  // (r, c) missing at its batch start)
-  out.blast.assign(w, -1);
-  for (size_t b = 0; b < out.bat.size(); b++)
-    for (size_t q = out.bat[b].q0; q < out.bat[b].q1; q++) {
-      if (ops[q].axis == CDA_AXIS_ROW) {
-        out.blast[ops[q].idx] = (int)b;
-        continue;
-      }
-      const uint8_t* pr = pres_out + q * W;
-      for (int j = 0; j < w; j++)
-        if (!pr[j]) out.blast[j] = (int)b;
-    }
   return CDA_OK;
 }
 

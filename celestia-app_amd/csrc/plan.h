@@ -36,7 +36,26 @@ struct Presence {
     for (int wd = 0; wd < words; wd++)
       for (uint64_t m = ~b[wd] & full; m; m &= m - 1) f(wd * 64 + __builtin_ctzll(m));
   }
-  void fill(int a, int idx);                         // mark every cell of axis (a, idx) present
+  // mark every cell of axis (a, idx) present; f(o, j, n) for each cell (a, idx) x (o = 1 - a, j) that was
+  // missing, n = axis (o, j)'s new count, j ascending
+  template <class F>
+  void fill(int a, int idx, F f) {
+    const int o = 1 - a;
+    uint64_t* b = bits[a].data() + (size_t)idx * words;
+    const uint64_t bit = 1ull << (idx & 63);
+    for (int wd = 0; wd < words; wd++) {
+      for (uint64_t m = ~b[wd] & full; m; m &= m - 1) {
+        const int j = wd * 64 + __builtin_ctzll(m);
+        bits[o][(size_t)j * words + (idx >> 6)] |= bit;
+        f(o, j, ++cnt[o][j]);
+      }
+      b[wd] = full;
+    }
+    cnt[a][idx] = w;
+  }
+  void fill(int a, int idx) {
+    fill(a, idx, [](int, int, int) {});
+  }
   void bytes(int a, int idx, uint8_t* out) const;  // presence of axis (a, idx)'s cells, one byte (0/1) each
 };
 

@@ -105,15 +105,73 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   const unsigned* bfl = (const unsigned*)(h + o_bfl);
   const unsigned* sfl = (const unsigned*)(h + o_sfl);
   const unsigned* pfl = (const unsigned*)(h + o_pfl);
-  // The EDS upload (pageable memory: the copy occupies the calling thread) runs on a helper thread
-  // while this one plans the whole repair on the presence bitsets.
+  Presence P;
+  P.init(w, present);
+  // The EDS upload (pageable memory: the copy occupies the calling thread) runs on a helper thread while this
+  // one plans the whole repair on the presence bitsets.  A sparse square (e.g. Q0 only: 25 % of the bytes) goes
+  // up as its runs of present cells only (gaps of < 8 missing cells are sent along), packed through the pinned
+  // ring into rcompact and scattered into place on the device; its missing cells are zeroed there first, so a
+  // failed repair hands back zeros, not a previous square's bytes, in the cells it could not fill.
+  std::vector<HostRun> runs;
+  std::vector<uint32_t> run_tab;  // dst cell of each run, then the packed prefix (nruns + 1)
+  size_t packed_cells = 0;
+  if (eds) {
+    constexpr uint32_t kGap = 8;
+    const uint32_t ncells = (uint32_t)(W * W);
+    std::vector<std::pair<uint32_t, uint32_t>> cr;  // (first cell, cells)
+    size_t npresent = 0;
+    for (int r = 0; r < w; r++) npresent += P.cnt[CDA_AXIS_ROW][r];
+    // runs of present cells in row-major order, word by word; a gap of < kGap cells joins two runs
+    for (int r = 0; r < w && npresent * 4 <= (size_t)ncells * 3 && cr.size() <= (1u << 16); r++) {
+      const uint64_t* b = P.bits[CDA_AXIS_ROW].data() + (size_t)r * P.words;
+      for (int wd = 0; wd < P.words; wd++) {
+        uint64_t m = b[wd] & P.full;
+        while (m) {
+          const int lo = __builtin_ctzll(m);
+          const uint64_t above = ~m >> lo;  // the run of set bits starting at lo
+          const int len = above ? __builtin_ctzll(above) : 64 - lo;
+          const uint32_t g0 = (uint32_t)r * w + wd * 64 + lo;
+          if (!cr.empty() && g0 - (cr.back().first + cr.back().second) < kGap)
+            cr.back().second = g0 + len - cr.back().first;
+          else
+            cr.emplace_back(g0, (uint32_t)len);
+          m = lo + len >= 64 ? 0 : m & (~0ull << (lo + len));
+        }
+      }
+    }
+    for (auto& x : cr) packed_cells += x.second;
+    if (npresent * 4 <= (size_t)ncells * 3 && packed_cells * 4 <= (size_t)ncells * 3 && cr.size() <= (1u << 16)) {
+      runs.reserve(cr.size());
+      run_tab.resize(2 * cr.size() + 1);
+      uint32_t pre = 0;
+      for (size_t i = 0; i < cr.size(); i++) {
+        runs.push_back(HostRun{(size_t)cr[i].first * CDA_SHARE, (size_t)cr[i].second * CDA_SHARE});
+        run_tab[i] = cr[i].first;
+        run_tab[cr.size() + i] = pre;
+        pre += cr[i].second;
+      }
+      run_tab[2 * cr.size()] = pre;
+    } else {
+      packed_cells = 0;
+    }
+  }
+  const bool packed = !runs.empty();
+  if (packed) {
+    if ((rc = ensure(c, c->rcompact, packed_cells * CDA_SHARE)) || (rc = ensure(c, c->rruns, run_tab.size() * 4)))
+      return rc;
+    if (!dev_ok(c, hipMemcpyAsync(c->rruns.p, run_tab.data(), run_tab.size() * 4, hipMemcpyHostToDevice, s), "H2D") ||
+        !dev_ok(c, hipMemsetAsync(d_eds, 0, eds_b, s), "memset"))
+      return CDA_E_DEVICE;
+  }
   bool h2d_ok = true;
   std::thread h2d;
   if (eds)
     h2d = std::thread([&] {
       try {
         (void)hipSetDevice(c->device);
-        h2d_ok = staged_h2d(c, d_eds, eds, eds_b, s) == CDA_OK;
+        bind_helper_thread(c);
+        h2d_ok = (packed ? staged_h2d_runs(c, c->rcompact.p, eds, runs.data(), runs.size(), s)
+                         : staged_h2d(c, d_eds, eds, eds_b, s)) == CDA_OK;
       } catch (...) {  // nothing may escape a helper thread (std::terminate)
         (void)api_exception(c);
         h2d_ok = false;
@@ -130,8 +188,6 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   } joiner{h2d, s};
   RepairTrace tr;
   tr.mark("setup");
-  Presence P;
-  P.init(w, present);
   const uint8_t* want[2] = {row_roots, col_roots};
 
   // ---- plan: prerepairSanityCheck axes, then every crossword sweep on the optimistic presence (plan.cpp) ----
@@ -176,6 +232,12 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   if (!h2d_ok) {
     c->last_err = "H2D failed";
     return CDA_E_DEVICE;
+  }
+  if (packed) {
+    const uint32_t* d_tab = (const uint32_t*)c->rruns.p;
+    const int nr = (int)runs.size();
+    if (launch_scatter_cell_runs(c->rcompact.p, d_eds, d_tab, d_tab + nr, nr, (uint32_t)packed_cells, s))
+      return CDA_E_DEVICE;
   }
   const int* d_ax = (const int*)(dd + o_ax);
   const int* d_sax = (const int*)(dd + o_sax);
@@ -353,6 +415,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     early_d2h = std::thread([&] {
       try {
         (void)hipSetDevice(c->device);
+        bind_helper_thread(c);
         hipStream_t d2h = c->d2h_stream;
         const size_t row_b = W * CDA_SHARE;
         for (size_t b = 0; b < nbat && !early_failed; b++) {

@@ -10,8 +10,13 @@
 // and the pageable copies were steady.  Pinned caller memory (cda_host_alloc, hipHostRegister) and small
 // copies go straight to hipMemcpyAsync.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -21,6 +26,59 @@
 #include "ctx.h"
 
 namespace cda {
+
+// NUMA placement of the helper threads (measured, scripts/c4_numa_probe.py: C4 host-buffer repair on threads of
+// the GPU's node 2.38 / 2.84 ms min / median, on the other socket 2.97 / 3.37 ms).
+void find_local_cpus(cda_ctx* c) {
+  c->local_cpus.clear();
+  if (const char* e = getenv("CDA_NUMA_BIND"))
+    if (atoi(e) == 0) return;
+  char bdf[64] = {};
+  if (hipDeviceGetPCIBusId(bdf, sizeof bdf, c->device) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  for (char* q = bdf; *q; q++) *q = (char)tolower((unsigned char)*q);
+  char path[160];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/local_cpulist", bdf);
+  FILE* f = fopen(path, "r");
+  if (!f) return;
+  char buf[4096] = {};
+  const size_t n = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+  for (char* q = buf; *q;) {  // "0-63,128-191"
+    char* end = nullptr;
+    const long a = strtol(q, &end, 10);
+    if (end == q) break;
+    long b = a;
+    if (*end == '-') {
+      q = end + 1;
+      b = strtol(q, &end, 10);
+    }
+    for (long x = a; x <= b && x < CPU_SETSIZE; x++)
+      if (x >= 0 && CPU_ISSET(x, &allowed)) c->local_cpus.push_back((int)x);
+    q = end;
+    while (*q == ',' || *q == '\n' || *q == ' ') q++;
+  }
+}
+
+void bind_helper_thread(const cda_ctx* c) {
+  if (c->local_cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int x : c->local_cpus) CPU_SET(x, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);  // best effort: placement, not correctness
+}
+
+struct Piece {
+  uint8_t* dst;
+  const uint8_t* src;
+  size_t n;
+};
 
 struct Stager {
   static constexpr int kSlots = 3;
@@ -32,17 +90,28 @@ struct Stager {
   std::vector<std::thread> th;
   std::mutex m;
   std::condition_variable cv_work, cv_done;
+  // the current job: one contiguous copy (jdst, jsrc, jn) or, with jp, the concatenation of jnp pieces
+  // (jn = their total bytes); part i of kWorkers + 1 copies bytes [jn * i / parts, jn * (i + 1) / parts)
   uint8_t* jdst = nullptr;
   const uint8_t* jsrc = nullptr;
-  size_t jn = 0;
+  const Piece* jp = nullptr;
+  size_t jn = 0, jnp = 0;
   unsigned gen = 0;
   int pending = 0;
   bool stop = false;
 
-  // part `i` of kWorkers + 1 of the current job
   void part(int i) {
     const size_t parts = kWorkers + 1, lo = jn * i / parts, hi = jn * (i + 1) / parts;
-    if (hi > lo) memcpy(jdst + lo, jsrc + lo, hi - lo);
+    if (hi <= lo) return;
+    if (!jp) {
+      memcpy(jdst + lo, jsrc + lo, hi - lo);
+      return;
+    }
+    size_t pos = 0;
+    for (size_t q = 0; q < jnp && pos < hi; pos += jp[q].n, q++) {
+      const size_t a = std::max(lo, pos), b = std::min(hi, pos + jp[q].n);
+      if (b > a) memcpy(jp[q].dst + (a - pos), jp[q].src + (a - pos), b - a);
+    }
   }
   void worker(int i) {
     unsigned seen = 0;
@@ -61,17 +130,9 @@ struct Stager {
       cv_done.notify_one();
     }
   }
-  // memcpy split over the workers and the calling thread
-  void pmemcpy(void* dst, const void* src, size_t n) {
-    if (n < ((size_t)256 << 10)) {
-      memcpy(dst, src, n);
-      return;
-    }
+  void run_job() {
     {
       std::lock_guard<std::mutex> g(m);
-      jdst = (uint8_t*)dst;
-      jsrc = (const uint8_t*)src;
-      jn = n;
       pending = kWorkers;
       ++gen;
     }
@@ -79,6 +140,26 @@ struct Stager {
     part(kWorkers);
     std::unique_lock<std::mutex> g(m);
     cv_done.wait(g, [&] { return pending == 0; });
+  }
+  // memcpy split over the workers and the calling thread
+  void pmemcpy(void* dst, const void* src, size_t n) {
+    if (n < ((size_t)256 << 10)) {
+      memcpy(dst, src, n);
+      return;
+    }
+    jdst = (uint8_t*)dst;
+    jsrc = (const uint8_t*)src;
+    jp = nullptr;
+    jn = n;
+    run_job();
+  }
+  // the pieces' bytes, split by position over the workers and the calling thread
+  void pgather(const Piece* p, size_t np, size_t total) {
+    jp = p;
+    jnp = np;
+    jn = total;
+    run_job();
+    jp = nullptr;
   }
   ~Stager() {
     {
@@ -106,7 +187,11 @@ static int get_stager(cda_ctx* c, Stager*& st) {
   }
   try {
     s->th.reserve(Stager::kWorkers);
-    for (int i = 0; i < Stager::kWorkers; i++) s->th.emplace_back([s, i] { s->worker(i); });
+    for (int i = 0; i < Stager::kWorkers; i++)
+      s->th.emplace_back([s, i, c] {
+        bind_helper_thread(c);
+        s->worker(i);
+      });
   } catch (...) {
     delete s;  // stops and joins the workers already started
     throw;
@@ -144,6 +229,39 @@ int staged_h2d(cda_ctx* c, void* d_dst, const void* h_src, size_t n, hipStream_t
     // the slot's previous DMA (chunk i - kSlots, or the last call's) has read it
     if (st.used[j] && !dev_ok(c, hipEventSynchronize(st.ev[j]), "staging wait")) return CDA_E_DEVICE;
     st.pmemcpy(slot, (const uint8_t*)h_src + off, len);
+    if (!dev_ok(c, hipMemcpyAsync((uint8_t*)d_dst + off, slot, len, hipMemcpyHostToDevice, s), "H2D") ||
+        !dev_ok(c, hipEventRecord(st.ev[j], s), "staging record"))
+      return CDA_E_DEVICE;
+    st.used[j] = true;
+  }
+  return CDA_OK;
+}
+
+int staged_h2d_runs(cda_ctx* c, void* d_dst, const uint8_t* h_base, const HostRun* runs, size_t nruns,
+                    hipStream_t s) {
+  size_t total = 0;
+  for (size_t i = 0; i < nruns; i++) total += runs[i].len;
+  if (total == 0) return CDA_OK;
+  int rc = get_stager(c, c->st_in);
+  if (rc) return rc;
+  Stager& st = *c->st_in;
+  const size_t B = Stager::kSlotBytes;
+  std::vector<Piece> pieces;
+  size_t r = 0, r_used = 0;  // next run, bytes of it already staged
+  for (size_t off = 0, i = 0; off < total; off += B, i++) {
+    const int j = (int)(i % Stager::kSlots);
+    const size_t len = std::min(B, total - off);
+    uint8_t* slot = st.ring + (size_t)j * B;
+    pieces.clear();
+    for (size_t fill = 0; fill < len;) {  // the next `len` bytes of the concatenated runs
+      const size_t take = std::min(len - fill, runs[r].len - r_used);
+      pieces.push_back(Piece{slot + fill, h_base + runs[r].off + r_used, take});
+      fill += take;
+      r_used += take;
+      if (r_used == runs[r].len) r++, r_used = 0;
+    }
+    if (st.used[j] && !dev_ok(c, hipEventSynchronize(st.ev[j]), "staging wait")) return CDA_E_DEVICE;
+    st.pgather(pieces.data(), pieces.size(), len);
     if (!dev_ok(c, hipMemcpyAsync((uint8_t*)d_dst + off, slot, len, hipMemcpyHostToDevice, s), "H2D") ||
         !dev_ok(c, hipEventRecord(st.ev[j], s), "staging record"))
       return CDA_E_DEVICE;

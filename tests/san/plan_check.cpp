@@ -68,9 +68,22 @@ static bool naive_crossword(std::vector<uint8_t> m, int w, int K, std::vector<Na
   }
 }
 
-static void check_repair(const std::vector<uint8_t>& present, int w, int K) {
+static void check_repair(const std::vector<uint8_t>& raw, int w, int K) {
   Presence P;
-  P.init(w, present.data());
+  P.init(w, raw.data());
+  std::vector<uint8_t> present(raw.size());
+  for (size_t i = 0; i < raw.size(); i++) present[i] = raw[i] != 0;
+  for (int a = 0; a < 2; a++)  // the bitsets and counts against the byte matrix
+    for (int i = 0; i < w; i++) {
+      int n = 0;
+      for (int j = 0; j < w; j++) {
+        const bool want = a == CDA_AXIS_ROW ? present[(size_t)i * w + j] != 0 : present[(size_t)j * w + i] != 0;
+        const bool got = (P.bits[a][(size_t)i * P.words + (j >> 6)] >> (j & 63)) & 1;
+        CHECK(want == got, "presence bit axis %d (%d, %d) (w=%d)", a, i, j, w);
+        n += want;
+      }
+      CHECK(P.cnt[a][i] == n, "presence count axis %d idx %d (w=%d)", a, i, w);
+    }
   RepairPlan rp;
   std::vector<uint8_t> pres(2 * (size_t)w * w, 0xAA);
   const int rc = plan_repair(P, K, rp, pres.data());
@@ -135,7 +148,7 @@ static void repair_cases(std::mt19937_64& rng) {
       std::vector<uint8_t> p((size_t)w * w);
       const int mode = r % 6;
       const double keep = mode == 0 ? 0.25 : mode == 1 ? 0.5 : mode == 2 ? 0.7 : 0.9;
-      for (auto& x : p) x = (rng() % 1000) < keep * 1000;
+      for (auto& x : p) x = (rng() % 1000) < keep * 1000 ? (uint8_t)(1 + rng() % 255) : 0;  // any nonzero byte = present
       if (mode == 4) {  // the minimal repairable pattern: Q0 present only
         for (int i = 0; i < w; i++)
           for (int j = 0; j < w; j++) p[(size_t)i * w + j] = i < k && j < k;

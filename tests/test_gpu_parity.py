@@ -341,6 +341,27 @@ def test_repair_random(ctx, k, frac):
     _check_repair(ctx, eds, rr, cr, pres)
 
 
+@pytest.mark.parametrize("k,frac", [(32, 0.3), (128, 0.2)])
+def test_repair_sparse_upload_leaves_zeros_where_unrepaired(ctx, k, frac):
+    """A square with <= 75 % of its cells present goes up as runs of present cells only (repair.cpp, packed
+    upload): an unrepairable one comes back with the oracle's presence and present cells, and zeros in every cell
+    still missing where the packed form was used, the caller's own bytes where the whole square went up -- never
+    bytes of an earlier square left on the device."""
+    eds, rr, cr = _square(k, 700 + k)
+    rng = np.random.default_rng(k)
+    pres = (rng.random(4 * k * k) < frac).astype(np.uint8)
+    ctx.repair_status(eds.copy(), np.ones_like(pres), rr, cr)  # leave a whole square in the device buffer
+    damaged = np.where(pres[:, None] == 1, eds, 0xEE).astype(np.uint8)
+    rc_o, eds_o, p_o, _, _ = O.repair(damaged, pres, rr, cr)
+    rc_g, eds_g, p_g, _ = ctx.repair_status(damaged, pres, rr, cr)
+    assert rc_g == rc_o == O.E_UNREPAIRABLE
+    assert np.array_equal(p_g, p_o)
+    m = p_o.astype(bool)
+    assert np.array_equal(eds_g[m], eds_o[m])
+    left = eds_g[~m]
+    assert np.all((left == 0) | (left == 0xEE))
+
+
 def test_repair_ff16(ctx):
     k = 256
     eds, rr, cr = _square(k, 7)
