@@ -119,22 +119,9 @@ __device__ __forceinline__ void xtime16(uint32_t (&T)[16]) {  // T *= x; x^16 = 
 // X ^= c * Y, c wave-uniform.  The bit tests are made to look lane-divergent (c copied into an opaque VGPR): the
 // compiler then guards each 16-XOR block with the exec mask, updating X in place, and skips the block with
 // s_cbranch_execz when the bit is clear.  As a scalar branch it renamed X in the taken block and paid 16 v_mov on the
-// other path, i.e. 16 VALU per bit either way.
+// other path, i.e. 16 VALU per bit either way.  A branch-free form (the bit as an all-ones VGPR mask, 16 v_bitop3 per
+// bit) was slower: columns 0.333 -> 0.369 ms per square (scripts/ab_rs16_uni.sh, round 3).
 __device__ __forceinline__ void muladd_uniform(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
-#if defined(CDA_RS16_UNI_MASK)
-  // branch-free variant (A/B): the bit of c as an all-ones / zero VGPR mask, 16 v_bitop3 per bit
-  uint32_t T[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) T[j] = Y[j];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe(c, i, 1);
-    asm volatile("" : "+v"(mk));
-#pragma unroll
-    for (int j = 0; j < 16; j++) X[j] = __builtin_amdgcn_bitop3_b32(X[j], T[j], mk, 0x78);
-    if (i < 15) xtime16(T);
-  }
-#else
   uint32_t cv = c;
   asm volatile("" : "+v"(cv));
   uint32_t T[16];
@@ -148,7 +135,6 @@ __device__ __forceinline__ void muladd_uniform(uint32_t (&X)[16], const uint32_t
     }
     if (i < 15) xtime16(T);
   }
-#endif
 }
 // X ^= c * Y, c per lane (16 lane masks)
 __device__ __forceinline__ void muladd_lane(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
