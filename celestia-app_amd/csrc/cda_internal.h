@@ -64,6 +64,10 @@ int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int
 int launch_nmt_trees(const void* d_leaves, void* d_levels, void* d_roots, int k, int nblocks, hipStream_t s,
                      void* prof_ctx);
 int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s);
+// every tree of nblocks blocks in one launch (LDS-resident), the DAH by the last workgroup of each block;
+// d_done: nblocks zeroed counters (left zeroed); d_digests: nblocks x 4k x 32 B scratch
+int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned* d_done, void* d_digests, int k,
+                     int nblocks, hipStream_t s);
 // single-axis tree (wrapper.NewConstructor tree of n leaves of 512 B)
 int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,
                      unsigned long long* d_status, hipStream_t s);

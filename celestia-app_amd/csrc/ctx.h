@@ -52,6 +52,7 @@ struct cda_ctx {
     size_t cap = 0;
   };
   Buf ods, eds, leaf, scratch, roots, dah, status, plan, payload;
+  Buf done;  // per-block tree counters of the small-batch tree launch (trees_lds_kernel), kept at zero
   // one square split over devices (split.cpp): this device's slab, row / column slabs, leaf records, send blocks,
   // tree scratch, per-device results (meta) and, on the first device, the gathered results
   Buf sp_ods, sp_R, sp_LR, sp_S, sp_C, sp_LC, sp_scratch, sp_meta, sp_gather;
@@ -81,6 +82,8 @@ namespace cda {
 // Largest ODS width on the device block path: FF16 codewords up to m = 2048 in
 // LDS, DAH tree of 4k roots in one workgroup's LDS (k <= 512).
 constexpr uint32_t kMaxDeviceK = 512;
+// batches of at most this many trees (B x 2w) take the one-launch LDS tree path (enqueue_trees; CDA_TREES_LDS)
+constexpr int kLdsTreesMax = 512;
 
 bool dev_ok(cda_ctx* c, hipError_t e, const char* what);
 int ensure(cda_ctx* c, cda_ctx::Buf& b, size_t bytes);

@@ -208,6 +208,21 @@ int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, u
 // NMT levels + DAH of nblocks blocks whose leaf records are at record offset rec_off.
 int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void* d_dah, hipStream_t s, size_t rec_off) {
   const uint32_t w = 2 * k;
+  // small batches (latency: the consensus path extends one block): all trees + the DAH in one LDS-resident launch
+  static const int lds_trees = getenv("CDA_TREES_LDS") ? atoi(getenv("CDA_TREES_LDS")) : kLdsTreesMax;
+  if ((size_t)nblocks * 2 * w <= (size_t)lds_trees && w <= 256) {
+    const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255, need = cnt_b + (size_t)nblocks * 2 * w * 32;
+    if (c->done.cap < need) {  // counters zeroed once (the kernel leaves them at 0), then the digest scratch
+      int rc = ensure(c, c->done, std::max<size_t>(need, 64 * 1024));
+      if (rc) return rc;
+      if (!dev_ok(c, hipMemsetAsync(c->done.p, 0, c->done.cap, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+    }
+    ProfScope ps(c, "trees_lds", s);
+    const int lr = launch_trees_lds((uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES, d_roots, d_dah,
+                                    (unsigned*)c->done.p, (uint8_t*)c->done.p + cnt_b, (int)k, (int)nblocks, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+    return CDA_OK;
+  }
   // inner levels in c->scratch: 2 records per leaf record of the chunk (2w x (w - 2) per block)
   const int lr0 = launch_nmt_trees((uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES,
                                    (uint8_t*)c->scratch.p + 2 * rec_off * CDA_REC_BYTES, d_roots, (int)k, (int)nblocks, s,
@@ -314,7 +329,7 @@ void cda_free(cda_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     flush_profile(c);
     for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status, &c->plan, &c->payload,
-                    &c->rdesc, &c->rcompact, &c->rruns, &c->sp_ods, &c->sp_R, &c->sp_LR, &c->sp_S, &c->sp_C, &c->sp_LC, &c->sp_scratch,
+                    &c->rdesc, &c->rcompact, &c->rruns, &c->done, &c->sp_ods, &c->sp_R, &c->sp_LR, &c->sp_S, &c->sp_C, &c->sp_LC, &c->sp_scratch,
                     &c->sp_meta, &c->sp_gather})
       if (b->p) (void)hipFree(b->p);
     for (auto e : c->sp_ev)

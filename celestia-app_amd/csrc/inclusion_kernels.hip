@@ -256,7 +256,7 @@ int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t
   const size_t lds = ((size_t)max_set + (max_set + 1) / 2) * 32;
   if (lds > 160 * 1024) return -2;
   if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)merkle_sets_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
   hipLaunchKernelGGL(merkle_sets_kernel, dim3(nsets), dim3(256), lds ? lds : 32, s, (const uint4*)d_recs, d_idx, d_off,
                      (uint32_t*)d_out, (uint32_t*)d_nodes_out);

@@ -245,4 +245,52 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
   for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
 }
 
+// hash_node_mem with both children already in registers (24 words each, record layout): the form for latency
+// kernels that run one wave per SIMD, where registers are free and a memory round trip per compression is not.
+__device__ __forceinline__ void hash_node_regs(const uint32_t (&L)[24], const uint32_t (&R)[24], uint32_t (&o)[24]) {
+  uint32_t st[8], m[16];
+  sha256_init(st);
+  m[0] = be_window(0x01000000u, L[0], 3);
+#pragma unroll
+  for (int i = 1; i < 16; i++) m[i] = be_window(L[i - 1], L[i], 3);
+  sha256_compress(st, m);
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int wi = 16 + i;
+    if (wi <= 21) m[i] = be_window(L[wi - 1], L[wi], 3);
+    else if (wi == 22) m[i] = be_window(L[21], L[22], 3) | (R[0] & 0xFFu);
+    else m[i] = be_window(R[wi - 23], R[wi - 22], 1);
+  }
+  sha256_compress(st, m);
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int wi = 32 + i;
+    if (wi <= 44) m[i] = be_window(R[wi - 23], R[wi - 22], 1);
+    else if (wi == 45) m[i] = be_window(R[22], R[23], 1) | 0x00800000u;
+    else if (wi == 46) m[i] = 0;
+    else m[i] = 181u * 8u;
+  }
+  sha256_compress(st, m);
+  bool rmin_max = true;
+#pragma unroll
+  for (int i = 0; i < 7; i++) rmin_max &= (R[i] == 0xFFFFFFFFu);
+  rmin_max &= ((R[7] & 0xFFu) == 0xFFu);
+  uint32_t S[16];
+#pragma unroll
+  for (int i = 7; i < 15; i++) S[i] = rmin_max ? L[i] : R[i];
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = bswap(st[i]);
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = L[i];
+  o[7] = (L[7] & 0xFFu) | (S[7] & 0xFFFFFF00u);
+#pragma unroll
+  for (int i = 8; i < 14; i++) o[i] = S[i];
+  o[14] = (S[14] & 0xFFFFu) | (d[0] << 16);
+#pragma unroll
+  for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
+  o[22] = d[7] >> 16;
+  o[23] = 0;
+}
+
 }  // namespace cda

@@ -19,6 +19,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "cda_internal.h"
 #include "nmt_dev.h"
@@ -185,34 +187,30 @@ int launch_nmt_trees(const void* d_leaves, void* d_levels, void* d_roots, int k,
 // Levels pair (2i, 2i+1) and promote an odd last node, which is the same tree as
 // HashFromByteSlices' "split at the largest power of two below n" recursion.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ roots, uint32_t* __restrict__ dah,
-                                                  int n) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t sdig[];  // [n + (n+1)/2][8] big-endian digests
-  const uint32_t blk = blockIdx.x;
-  const uint4* rb = roots + (size_t)blk * n * 6;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    uint32_t L[24];
-    load_node(rb + (size_t)i * 6, L);
-    uint32_t st[8], m[16];
-    sha256_init(st);
-    // 0x00 ‖ root[0..90) ‖ 0x80 ‖ ... ‖ len(91*8)
-    m[0] = be_window(0u, L[0], 3);
+// DAH leaf digest: SHA256(0x00 || root record[0..90)) as 8 big-endian words
+__device__ __forceinline__ void dah_leaf_digest(const uint32_t (&L)[24], uint32_t (&st)[8]) {
+  uint32_t m[16];
+  sha256_init(st);
+  // 0x00 ‖ root[0..90) ‖ 0x80 ‖ ... ‖ len(91*8)
+  m[0] = be_window(0u, L[0], 3);
 #pragma unroll
-    for (int t = 1; t < 16; t++) m[t] = be_window(L[t - 1], L[t], 3);
-    sha256_compress(st, m);
+  for (int t = 1; t < 16; t++) m[t] = be_window(L[t - 1], L[t], 3);
+  sha256_compress(st, m);
 #pragma unroll
-    for (int t = 0; t < 16; t++) {
-      const int wi = 16 + t;
-      if (wi <= 21) m[t] = be_window(L[wi - 1], L[wi], 3);
-      else if (wi == 22) m[t] = be_window(L[21], L[22], 3) | 0x80u;
-      else if (wi < 31) m[t] = 0;
-      else m[t] = 91u * 8u;
-    }
-    sha256_compress(st, m);
-#pragma unroll
-    for (int t = 0; t < 8; t++) sdig[i * 8 + t] = st[t];
+  for (int t = 0; t < 16; t++) {
+    const int wi = 16 + t;
+    if (wi <= 21) m[t] = be_window(L[wi - 1], L[wi], 3);
+    else if (wi == 22) m[t] = be_window(L[21], L[22], 3) | 0x80u;
+    else if (wi < 31) m[t] = 0;
+    else m[t] = 91u * 8u;
   }
-  __syncthreads();
+  sha256_compress(st, m);
+}
+
+// RFC-6962 levels over the n leaf digests at sdig ([n + (n+1)/2][8] words of LDS, the first n filled), by the
+// calling workgroup; the 32-B hash goes to out.  Levels pair (2i, 2i+1) and promote an odd last node, which is the
+// same tree as HashFromByteSlices' "split at the largest power of two below n" recursion.
+__device__ __forceinline__ void dah_fold(uint32_t* sdig, int n, uint32_t* out) {
   uint32_t* src = sdig;
   uint32_t* dst = sdig + n * 8;
   for (int cnt = n; cnt > 1;) {
@@ -249,7 +247,102 @@ __global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ root
     dst = tmp;
     cnt = out_cnt;
   }
-  if (threadIdx.x < 8) dah[blk * 8 + threadIdx.x] = bswap(src[threadIdx.x]);
+  if (threadIdx.x < 8) out[threadIdx.x] = bswap(src[threadIdx.x]);
+}
+
+// DAH: RFC-6962 over the n = 2w roots (rows then cols), one workgroup per block.
+__global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ roots, uint32_t* __restrict__ dah,
+                                                  int n) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sdig[];  // [n + (n+1)/2][8] big-endian digests
+  const uint4* rb = roots + (size_t)blockIdx.x * n * 6;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t L[24], st[8];
+    load_node(rb + (size_t)i * 6, L);
+    dah_leaf_digest(L, st);
+#pragma unroll
+    for (int t = 0; t < 8; t++) sdig[i * 8 + t] = st[t];
+  }
+  __syncthreads();
+  dah_fold(sdig, n, dah + blockIdx.x * 8);
+}
+
+// Small batches (the single block of ProcessProposal, config C2): every tree of the batch in ONE launch.  A
+// 256-thread workgroup takes two trees (waves 0-1 the first, waves 2-3 the second; one workgroup per CU at k = 128).
+// A tree's w leaf records go to LDS
+// (112-B stride: the 16-B reads of records two apart are bank-conflict free) and each level is computed into the
+// other half of a ping-pong pair, a thread holding both children in registers (hash_node_regs): a level costs its
+// 3 dependent compressions and a barrier, not a launch or a memory round trip per compression.  Each tree's root
+// then gets its DAH leaf digest; the workgroup that finishes a block's last tree pair (agent-scope acq_rel counter,
+// put back to 0 for the next call) folds the block's digests into the DAH, so the step needs no DAH launch.  The
+// batched form (nmt_levels_kernel + dah_kernel) keeps every lane on a useful node and stays the throughput path.
+constexpr int kLdsRec = 7;  // uint4 per LDS record
+__global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict__ leaves, uint4* __restrict__ roots,
+                                                        uint32_t* __restrict__ dah, unsigned* __restrict__ done,
+                                                        uint32_t* __restrict__ digests, int log2w) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // per half: A (w records) | B (w / 2); DAH reuses
+  __shared__ unsigned last;
+  const int w = 1 << log2w, n = 2 * w;
+  const int half = threadIdx.x >> 7, ht = threadIdx.x & 127;  // tree of this half, thread within it
+  const unsigned gtree = blockIdx.x * 2 + half;
+  const unsigned b = gtree >> (log2w + 1), tree = gtree & (n - 1);
+  const bool col = tree >= (unsigned)w;
+  const unsigned t = tree & (w - 1);
+  const uint4* lb = leaves + (size_t)b * w * w * 6;
+  if (threadIdx.x == 0) last = 0;  // published by the barrier after the leaf copy
+  uint4* A = lds + (size_t)half * (w + w / 2) * kLdsRec;
+  uint4* B = A + (size_t)w * kLdsRec;
+  for (int x = ht; x < w * 6; x += 128) {  // 16-B words of the w records, adjacent lanes adjacent
+    const int i = x / 6, q = x - i * 6;
+    const size_t rec = col ? ((size_t)i << log2w) + t : ((size_t)t << log2w) + i;
+    A[i * kLdsRec + q] = lb[rec * 6 + q];
+  }
+  __syncthreads();
+  for (int l = 1; l <= log2w; l++) {
+    const uint4* in = (l & 1) ? A : B;
+    uint4* out = (l & 1) ? B : A;
+    for (int i = ht; i < (w >> l); i += 128) {
+      uint32_t L[24], R[24], o[24];
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const uint4 u = in[(2 * i) * kLdsRec + q], v = in[(2 * i + 1) * kLdsRec + q];
+        L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
+        R[4 * q] = v.x, R[4 * q + 1] = v.y, R[4 * q + 2] = v.z, R[4 * q + 3] = v.w;
+      }
+      hash_node_regs(L, R, o);
+#pragma unroll
+      for (int q = 0; q < 6; q++) out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    }
+    __syncthreads();
+  }
+  const uint4* root = (log2w & 1) ? B : A;
+  uint4* rout = roots + ((size_t)b * n + tree) * 6;
+  if (ht < 6) rout[ht] = root[ht];
+  if (ht == 0) {  // this root's DAH leaf digest
+    uint32_t L[24], st[8];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const uint4 u = root[q];
+      L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
+    }
+    dah_leaf_digest(L, st);
+    uint4* dg = reinterpret_cast<uint4*>(digests + ((size_t)b * n + tree) * 8);
+    dg[0] = make_uint4(st[0], st[1], st[2], st[3]);
+    dg[1] = make_uint4(st[4], st[5], st[6], st[7]);
+  }
+  __syncthreads();  // both halves' roots and digests are stored (each by lanes of the wave that increments below)
+  if (threadIdx.x == 0 || threadIdx.x == 128) {  // one increment per tree, from the wave that stored it
+    const unsigned prev = __hip_atomic_fetch_add(done + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)n - 1) last = 1;  // at most one tree of a block is its last
+  }
+  __syncthreads();
+  if (!last) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the other workgroups' digests (released before their increments)
+  uint32_t* sdig = reinterpret_cast<uint32_t*>(lds);
+  const uint4* src = reinterpret_cast<const uint4*>(digests + (size_t)b * n * 8);
+  for (int x = threadIdx.x; x < n * 2; x += blockDim.x) reinterpret_cast<uint4*>(sdig)[x] = src[x];
+  __syncthreads();
+  dah_fold(sdig, n, dah + b * 8);
+  if (threadIdx.x == 0) __hip_atomic_store(done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -356,12 +449,33 @@ int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned* d_done, void* d_digests, int k,
+                     int nblocks, hipStream_t s) {
+  const int w = 2 * k;
+  int log2w = 0;
+  while ((1 << log2w) < w) log2w++;
+  if ((1 << log2w) != w || log2w < 1) return -2;
+  if (w > 256) return -2;  // a thread per node of level 1 within a 128-thread half
+  // two trees x (w + w / 2) records of 112 B; >= (2w + w) x 32 B of DAH digests
+  const size_t lds = 2 * ((size_t)w + w / 2 + 1) * kLdsRec * 16;
+  // the dynamic-LDS limit is raised to what the launch needs: 160 KiB would exceed the CU's LDS by the kernel's
+  // static __shared__ word and the call would fail (and with it the launch)
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)trees_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(trees_lds_kernel, dim3((unsigned)nblocks * w), dim3(256), lds, s,
+                     (const uint4*)d_leaves, (uint4*)d_roots, (uint32_t*)d_dah, d_done, (uint32_t*)d_digests, log2w);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s) {
   if (n_roots_total < 1) return -2;
   const size_t lds = ((size_t)n_roots_total + (n_roots_total + 1) / 2) * 32;
   if (lds > 160 * 1024) return -2;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)dah_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)dah_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -1;
   hipLaunchKernelGGL(dah_kernel, dim3(nblocks), dim3(256), lds, s, (const uint4*)d_roots, (uint32_t*)d_dah,
                      n_roots_total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -516,9 +630,10 @@ int launch_axes_verify(const uint8_t* d_eds, int k, const int* d_axes, int ntree
   while ((1 << log2w) < 2 * k) log2w++;
   const size_t lds = ((size_t)2 * k) * CDA_REC_BYTES;
   if (lds > 160 * 1024) return -2;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)axes_verify_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)axes_verify_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return -1;
   hipLaunchKernelGGL(axes_verify_kernel, dim3(ntrees), dim3(256), lds, s, d_eds, k, log2w, d_axes, d_want_rows,
                      d_want_cols, d_flag, base, per_tree ? 1 : 0);
   return hipGetLastError() == hipSuccess ? 0 : -1;

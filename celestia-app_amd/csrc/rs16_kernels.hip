@@ -120,7 +120,7 @@ __device__ __forceinline__ void xtime16(uint32_t (&T)[16]) {  // T *= x; x^16 = 
 // compiler then guards each 16-XOR block with the exec mask, updating X in place, and skips the block with
 // s_cbranch_execz when the bit is clear.  As a scalar branch it renamed X in the taken block and paid 16 v_mov on the
 // other path, i.e. 16 VALU per bit either way.  A branch-free form (the bit as an all-ones VGPR mask, 16 v_bitop3 per
-// bit) was slower: columns 0.333 -> 0.369 ms per square (scripts/ab_rs16_uni.sh, round 3).
+// bit) was slower: columns 0.333 -> 0.369 ms per square (round-3 A/B on one box).
 __device__ __forceinline__ void muladd_uniform(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
   uint32_t cv = c;
   asm volatile("" : "+v"(cv));
