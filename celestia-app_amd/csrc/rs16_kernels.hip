@@ -26,6 +26,12 @@
 // in wave bits it is wave-uniform (runtime: scalar branches on its 16 bits); when some sit in lane bits (d <= 2) it
 // is per lane (16 lane masks x 16 planes, v_bitop3).  The old LDS encoder paid the per-lane form on 12 of 18 layers
 // and one LDS round trip + barrier per layer; here 6 of 18 layers are per-lane and the state crosses LDS 4 times.
+//
+// Wave bits W2, W3 are made compile-time by running one kernel body per value (scalar branch at entry), so layers
+// 5..8 (LD, LE) multiply by compile-time constants.  In LC the layer-3/4 constants still depend on W0, W1 (p5, p6).
+// Leopard's skews are GF(2)-affine in the position bits (FFTSkew[j + 2^(i+1)] = FFTSkew[j] ^ temp[i] in
+// FFTInitialize; checked for every layer in tests/test_rs16_affine.py), so such a constant is c_ct ^ w0*t5 ^ w1*t6
+// with c_ct, t5, t6 compile-time: one XOR program plus one more per set runtime bit, no per-bit scalar branches.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -116,26 +122,6 @@ __device__ __forceinline__ void xtime16(uint32_t (&T)[16]) {  // T *= x; x^16 = 
   T[3] ^= t;
   T[5] ^= t;
 }
-// X ^= c * Y, c wave-uniform.  The bit tests are made to look lane-divergent (c copied into an opaque VGPR): the
-// compiler then guards each 16-XOR block with the exec mask, updating X in place, and skips the block with
-// s_cbranch_execz when the bit is clear.  As a scalar branch it renamed X in the taken block and paid 16 v_mov on the
-// other path, i.e. 16 VALU per bit either way.  A branch-free form (the bit as an all-ones VGPR mask, 16 v_bitop3 per
-// bit) was slower: columns 0.333 -> 0.369 ms per square (round-3 A/B on one box).
-__device__ __forceinline__ void muladd_uniform(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
-  uint32_t cv = c;
-  asm volatile("" : "+v"(cv));
-  uint32_t T[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) T[j] = Y[j];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    if ((cv >> i) & 1u) {
-#pragma unroll
-      for (int j = 0; j < 16; j++) X[j] ^= T[j];
-    }
-    if (i < 15) xtime16(T);
-  }
-}
 // X ^= c * Y, c per lane (16 lane masks)
 __device__ __forceinline__ void muladd_lane(uint32_t (&X)[16], const uint32_t (&Y)[16], unsigned c) {
   uint32_t T[16];
@@ -182,6 +168,17 @@ __device__ __forceinline__ int pos_wave(const Lay& Y, int w) {
     if (Y.s[b] >= 8) p |= ((w >> (Y.s[b] - 8)) & 1) << b;
   return p;
 }
+constexpr int pos_w_ct(const Lay& Y, int wv) {  // position bits of wave index wv (compile-time)
+  int p = 0;
+  for (int b = 0; b < L; b++)
+    if (Y.s[b] >= 8 && ((wv >> (Y.s[b] - 8)) & 1)) p |= 1 << b;
+  return p;
+}
+constexpr int pos_of_slot(const Lay& Y, int slot) {  // the position bit held by a slot
+  for (int b = 0; b < L; b++)
+    if (Y.s[b] == slot) return b;
+  return -1;
+}
 constexpr bool bits_above_in(const Lay& Y, int d, int lo, int hi) {  // any position bit > d in slots [lo, hi)
   for (int b = d + 1; b < L; b++)
     if (Y.s[b] >= lo && Y.s[b] < hi) return true;
@@ -194,17 +191,28 @@ constexpr bool bits_above_in(const Lay& Y, int d, int lo, int hi) {  // any posi
 constexpr int lv_slot(bool inv, int d, int r) {  // r = the butterfly's lower register index
   return (inv ? 0 : 6) + (inv ? d : 2 - d) * 2 + ((r & 1) | (r >> 1));
 }
-// The 16 wave-uniform constants (layers d = 3..6 of both transforms) likewise, into SGPRs.
-constexpr int un_slot(bool inv, int d, int r) { return (inv ? 0 : 8) + (d - 3) * 2 + ((r & 1) | (r >> 1)); }
 struct Ctx {
   const uint16_t* cpoly;  // alpha^skew[i] in the standard basis, 0 = no multiply
   int lane, w;
   uint32_t lv[6];         // packed per-lane constants, slot lv_slot(..)
-  uint32_t un[8];         // packed wave-uniform constants, slot un_slot(..)
 };
 
 // One butterfly of layer d (bit d in register slot RB of layout Y) between E[R] and E[R | 1 << RB].
-template <const Lay& Y, bool INVERSE, int D, int R>
+// layer constant index for group start s0 (bits above d of the position)
+template <bool INVERSE, int D>
+constexpr int cidx(int s0) {
+  return INVERSE ? (M - 1 + s0 + (1 << D)) : (s0 + (1 << D) - 1);
+}
+// X ^= t * Y for the runtime wave bit in slot SLOT (position bit P) if that bit of w is set: t = g(2^P) ^ g(0) with
+// g the layer's constant as a function of the group start.  The bit test is made to look lane-divergent (opaque
+// VGPR copy of w), so the compiler guards the XOR program with the exec mask and updates X in place (a scalar
+// branch renamed X and paid copies on the other path).
+template <bool INVERSE, int D, int SLOT, int P>
+__device__ __forceinline__ void muladd_wbit(uint32_t (&X)[16], const uint32_t (&Yv)[16], uint32_t wv) {
+  constexpr unsigned t = kCpoly16[cidx<INVERSE, D>(1 << P)] ^ kCpoly16[cidx<INVERSE, D>(0)];
+  if ((wv >> (SLOT - 8)) & 1u) muladd_const<t>(X, Yv);
+}
+template <const Lay& Y, bool INVERSE, int D, int R, int OM>
 __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
   constexpr int RB = Y.s[D];
   static_assert(RB == 0 || RB == 1, "butterfly bit must sit in a register slot");
@@ -212,8 +220,6 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
     uint32_t(&X)[16] = E[R];
     uint32_t(&Yv)[16] = E[R | (1 << RB)];
     constexpr int hi = ~((2 << D) - 1);
-    constexpr int s0r = pos_r(Y, R) & hi;
-    constexpr int base = INVERSE ? (M - 1 + s0r + (1 << D)) : (s0r + (1 << D) - 1);
     if (INVERSE) {
 #pragma unroll
       for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
@@ -221,13 +227,17 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
     if constexpr (bits_above_in(Y, D, 3, 8)) {  // per-lane constant (preloaded)
       constexpr int slot = lv_slot(INVERSE, D, R);
       muladd_lane(X, Yv, (cx.lv[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu);
-    } else if constexpr (bits_above_in(Y, D, 8, 16)) {  // wave-uniform constant (preloaded)
-      constexpr int slot = un_slot(INVERSE, D, R);
-      const unsigned c = (cx.un[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu;
-      if (c) muladd_uniform(X, Yv, c);
-    } else {  // compile-time constant
-      static_assert(base < kCpoly16N, "constant table too short");
-      muladd_const<kCpoly16[base]>(X, Yv);
+    } else {  // compile-time, plus one term per runtime wave bit (W0, W1) above d
+      constexpr int sct = (pos_r(Y, R) + pos_w_ct(Y, OM * 4)) & hi;
+      static_assert(cidx<INVERSE, D>(sct) < kCpoly16N, "constant table too short");
+      muladd_const<kCpoly16[cidx<INVERSE, D>(sct)]>(X, Yv);
+      constexpr int p8 = pos_of_slot(Y, 8), p9 = pos_of_slot(Y, 9);
+      if constexpr (p8 > D || p9 > D) {
+        uint32_t wv = cx.w;
+        asm volatile("" : "+v"(wv));
+        if constexpr (p8 > D) muladd_wbit<INVERSE, D, 8, p8>(X, Yv, wv);
+        if constexpr (p9 > D) muladd_wbit<INVERSE, D, 9, p9>(X, Yv, wv);
+      }
     }
     if (!INVERSE) {
 #pragma unroll
@@ -235,12 +245,12 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
     }
   }
 }
-template <const Lay& Y, bool INVERSE, int D>
+template <const Lay& Y, bool INVERSE, int D, int OM>
 __device__ __forceinline__ void layer(uint32_t (&E)[4][16], const Ctx& cx) {
-  butterfly<Y, INVERSE, D, 0>(E, cx);
-  butterfly<Y, INVERSE, D, 1>(E, cx);
-  butterfly<Y, INVERSE, D, 2>(E, cx);
-  butterfly<Y, INVERSE, D, 3>(E, cx);
+  butterfly<Y, INVERSE, D, 0, OM>(E, cx);
+  butterfly<Y, INVERSE, D, 1, OM>(E, cx);
+  butterfly<Y, INVERSE, D, 2, OM>(E, cx);
+  butterfly<Y, INVERSE, D, 3, OM>(E, cx);
 }
 
 template <const Lay& Y, bool INVERSE, int D, int R>
@@ -252,23 +262,6 @@ __device__ __forceinline__ void lv_fetch(Ctx& cx) {
   static_assert(!((R >> RB) & 1), "R is the lower register of its butterfly");
   const uint32_t c = cx.cpoly[base + ((pos_lane(Y, cx.lane) + pos_wave(Y, cx.w)) & hi)];
   cx.lv[slot >> 1] |= c << (16 * (slot & 1));
-}
-template <const Lay& Y, bool INVERSE, int D, int R>
-__device__ __forceinline__ uint32_t un_fetch(const Ctx& cx) {
-  constexpr int hi = ~((2 << D) - 1);
-  constexpr int base = INVERSE ? (M - 1 + (pos_r(Y, R) & hi) + (1 << D)) : ((pos_r(Y, R) & hi) + (1 << D) - 1);
-  return cx.cpoly[base + (pos_wave(Y, cx.w) & hi)];
-}
-template <bool INVERSE>
-__device__ __forceinline__ void un_fetch_dir(Ctx& cx) {
-  const uint32_t c[8] = {un_fetch<LC, INVERSE, 3, 0>(cx), un_fetch<LC, INVERSE, 3, 1>(cx),
-                         un_fetch<LC, INVERSE, 4, 0>(cx), un_fetch<LC, INVERSE, 4, 2>(cx),
-                         un_fetch<LD, INVERSE, 5, 0>(cx), un_fetch<LD, INVERSE, 5, 2>(cx),
-                         un_fetch<LD, INVERSE, 6, 0>(cx), un_fetch<LD, INVERSE, 6, 1>(cx)};
-  static_assert(un_slot(INVERSE, 6, 1) - un_slot(INVERSE, 3, 0) == 7, "slot order");
-  constexpr int s0 = un_slot(INVERSE, 3, 0) >> 1;
-#pragma unroll
-  for (int i = 0; i < 4; i++) cx.un[s0 + i] = __builtin_amdgcn_readfirstlane(c[2 * i] | (c[2 * i + 1] << 16));
 }
 __device__ __forceinline__ void lv_fetch_all(Ctx& cx) {
 #pragma unroll
@@ -376,10 +369,9 @@ struct Args {
   int mode;  // diagnostics (CDA_RS16_MODE): 0 = encode; 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores
 };
 
-__global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
+template <int OM>  // the body of the waves with (W3, W2) = OM
+__device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int wg = blockIdx.x;
   const int slice = wg % a.slices;
   wg /= a.slices;
@@ -389,10 +381,8 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
   uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
   uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
-  Ctx cx{a.cpoly, lane, w, {}, {}};
+  Ctx cx{a.cpoly, lane, w, {}};
   lv_fetch_all(cx);
-  un_fetch_dir<true>(cx);
-  un_fetch_dir<false>(cx);
   uint32_t lm3 = ((lane >> 3) & 1) ? ~0u : 0u;
   asm volatile("" : "+v"(lm3));
 
@@ -429,33 +419,33 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   }
   if (a.mode == 1) goto store;
   // IFFT, D = 1 .. m/2
-  layer<LA, true, 0>(E, cx);
-  layer<LA, true, 1>(E, cx);
+  layer<LA, true, 0, OM>(E, cx);
+  layer<LA, true, 1, OM>(E, cx);
   swap_lane45(E);
-  layer<LB, true, 2>(E, cx);
+  layer<LB, true, 2, OM>(E, cx);
   swap_lane3(E, lm3);
-  layer<LC, true, 3>(E, cx);
-  layer<LC, true, 4>(E, cx);
+  layer<LC, true, 3, OM>(E, cx);
+  layer<LC, true, 4, OM>(E, cx);
   exchange_w<0>(E, xb, w, lane);
-  layer<LD, true, 5>(E, cx);
-  layer<LD, true, 6>(E, cx);
+  layer<LD, true, 5, OM>(E, cx);
+  layer<LD, true, 6, OM>(E, cx);
   exchange_w<1>(E, xb, w, lane);
-  layer<LE, true, 7>(E, cx);
-  layer<LE, true, 8>(E, cx);
+  layer<LE, true, 7, OM>(E, cx);
+  layer<LE, true, 8, OM>(E, cx);
   // FFT, D = m/2 .. 1
-  layer<LE, false, 8>(E, cx);
-  layer<LE, false, 7>(E, cx);
+  layer<LE, false, 8, OM>(E, cx);
+  layer<LE, false, 7, OM>(E, cx);
   exchange_w<1>(E, xb, w, lane);
-  layer<LD, false, 6>(E, cx);
-  layer<LD, false, 5>(E, cx);
+  layer<LD, false, 6, OM>(E, cx);
+  layer<LD, false, 5, OM>(E, cx);
   exchange_w<0>(E, xb, w, lane);
-  layer<LC, false, 4>(E, cx);
-  layer<LC, false, 3>(E, cx);
+  layer<LC, false, 4, OM>(E, cx);
+  layer<LC, false, 3, OM>(E, cx);
   swap_lane3(E, lm3);
-  layer<LB, false, 2>(E, cx);
+  layer<LB, false, 2, OM>(E, cx);
   swap_lane45(E);
-  layer<LA, false, 1>(E, cx);
-  layer<LA, false, 0>(E, cx);
+  layer<LA, false, 1, OM>(E, cx);
+  layer<LA, false, 0, OM>(E, cx);
 store:
   if (a.mode == 3 && blockIdx.x != 0x7FFFFFFF) return;
   // parity shard s = point s
@@ -480,6 +470,19 @@ store:
     o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
     o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
     o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+  }
+}
+
+// one whole body per value of W2, W3 (scalar branch at entry; each runs to the end, so no control-flow merge with
+// the 64 live state registers follows the specialised layers -- such a merge made the register allocator spill)
+__global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  switch (w >> 2) {
+    case 0: body<0>(a, xb, w); break;
+    case 1: body<1>(a, xb, w); break;
+    case 2: body<2>(a, xb, w); break;
+    default: body<3>(a, xb, w); break;
   }
 }
 
