@@ -185,16 +185,17 @@ constexpr bool bits_above_in(const Lay& Y, int d, int lo, int hi) {  // any posi
   return false;
 }
 
-// The 12 per-lane constants (layers d = 0, 1, 2 of both transforms, two butterflies each) are fetched once at the
-// start, together with the data, two 16-bit values per VGPR: fetched at their layer, each would stall its wave on a
-// global-load round trip inside the compute phase.
+// The 8 generic per-lane constants (layers d = 0, 1 of both transforms, two butterflies each) are fetched once at
+// the start, together with the data, two 16-bit values per VGPR: fetched at their layer, each would stall its wave on
+// a global-load round trip inside the compute phase.
 constexpr int lv_slot(bool inv, int d, int r) {  // r = the butterfly's lower register index
-  return (inv ? 0 : 6) + (inv ? d : 2 - d) * 2 + ((r & 1) | (r >> 1));
+  return (inv ? 0 : 4) + (inv ? d : 1 - d) * 2 + ((r & 1) | (r >> 1));
 }
 struct Ctx {
   const uint16_t* cpoly;  // alpha^skew[i] in the standard basis, 0 = no multiply
   int lane, w;
-  uint32_t lv[6];         // packed per-lane constants, slot lv_slot(..)
+  uint32_t lv[4];         // packed per-lane constants, slot lv_slot(..)
+  uint32_t lm3;           // all-ones in lanes with lane bit 3 set
 };
 
 // One butterfly of layer d (bit d in register slot RB of layout Y) between E[R] and E[R | 1 << RB].
@@ -212,6 +213,24 @@ __device__ __forceinline__ void muladd_wbit(uint32_t (&X)[16], const uint32_t (&
   constexpr unsigned t = kCpoly16[cidx<INVERSE, D>(1 << P)] ^ kCpoly16[cidx<INVERSE, D>(0)];
   if ((wv >> (SLOT - 8)) & 1u) muladd_const<t>(X, Yv);
 }
+// X ^= (C * Y) & mk, C compile-time
+template <unsigned C, int I = 0>
+__device__ __forceinline__ void muladd_const_masked(uint32_t (&X)[16], const uint32_t (&Y)[16], uint32_t mk) {
+  if constexpr (C != 0 && I < 16) {
+    constexpr unsigned ROW = mul_row(C, I);
+    if constexpr (ROW != 0) {
+      const uint32_t z = fold_row<ROW, 0, -1>(0u, Y);
+      X[I] = __builtin_amdgcn_bitop3_b32(X[I], z, mk, 0x78);  // X ^ (z & mk)
+    }
+    muladd_const_masked<C, I + 1>(X, Y, mk);
+  }
+}
+constexpr int lane_bits_above(const Lay& Y, int d) {
+  int n = 0;
+  for (int b = d + 1; b < L; b++)
+    if (Y.s[b] >= 3 && Y.s[b] < 8) n++;
+  return n;
+}
 template <const Lay& Y, bool INVERSE, int D, int R, int OM>
 __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
   constexpr int RB = Y.s[D];
@@ -224,10 +243,10 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
 #pragma unroll
       for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
     }
-    if constexpr (bits_above_in(Y, D, 3, 8)) {  // per-lane constant (preloaded)
+    if constexpr (lane_bits_above(Y, D) > 1) {  // per-lane constant (preloaded), generic multiply
       constexpr int slot = lv_slot(INVERSE, D, R);
       muladd_lane(X, Yv, (cx.lv[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu);
-    } else {  // compile-time, plus one term per runtime wave bit (W0, W1) above d
+    } else {  // compile-time, plus one term per runtime wave bit (W0, W1) and lane bit 3 above d
       constexpr int sct = (pos_r(Y, R) + pos_w_ct(Y, OM * 4)) & hi;
       static_assert(cidx<INVERSE, D>(sct) < kCpoly16N, "constant table too short");
       muladd_const<kCpoly16[cidx<INVERSE, D>(sct)]>(X, Yv);
@@ -237,6 +256,12 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
         asm volatile("" : "+v"(wv));
         if constexpr (p8 > D) muladd_wbit<INVERSE, D, 8, p8>(X, Yv, wv);
         if constexpr (p9 > D) muladd_wbit<INVERSE, D, 9, p9>(X, Yv, wv);
+      }
+      if constexpr (lane_bits_above(Y, D) == 1) {  // a single lane bit (layer 2 in LB: p4 on lane bit 3)
+        constexpr int pl = pos_of_slot(Y, 3);
+        static_assert(pl > D, "the one lane bit above d is lane bit 3");
+        constexpr unsigned t = kCpoly16[cidx<INVERSE, D>(1 << pl)] ^ kCpoly16[cidx<INVERSE, D>(0)];
+        muladd_const_masked<t>(X, Yv, cx.lm3);
       }
     }
     if (!INVERSE) {
@@ -265,15 +290,11 @@ __device__ __forceinline__ void lv_fetch(Ctx& cx) {
 }
 __device__ __forceinline__ void lv_fetch_all(Ctx& cx) {
 #pragma unroll
-  for (int i = 0; i < 6; i++) cx.lv[i] = 0;
+  for (int i = 0; i < 4; i++) cx.lv[i] = 0;
   lv_fetch<LA, true, 0, 0>(cx);
   lv_fetch<LA, true, 0, 2>(cx);
   lv_fetch<LA, true, 1, 0>(cx);
   lv_fetch<LA, true, 1, 1>(cx);
-  lv_fetch<LB, true, 2, 0>(cx);
-  lv_fetch<LB, true, 2, 2>(cx);
-  lv_fetch<LB, false, 2, 0>(cx);
-  lv_fetch<LB, false, 2, 2>(cx);
   lv_fetch<LA, false, 1, 0>(cx);
   lv_fetch<LA, false, 1, 1>(cx);
   lv_fetch<LA, false, 0, 0>(cx);
@@ -365,111 +386,148 @@ struct Args {
   uint8_t* cpy;
   long long cpy_blk, cpy_cw, cpy_sh;
   const uint16_t* cpoly;
-  int cw_per_blk, slices;
+  int cw_per_blk, slices, total;  // total = codewords of the launch
   int mode;  // diagnostics (CDA_RS16_MODE): 0 = encode; 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores
 };
 
+typedef __attribute__((address_space(1))) void* glb_ptr;
+typedef __attribute__((address_space(3))) void* lds_ptr;
+
+// Persistent: workgroup blockIdx.x encodes codewords g = blockIdx.x, + gridDim.x, ... (one workgroup per CU: the
+// state fills the CU's registers, so a CU never holds a second codeword whose loads could overlap this one's
+// compute).  Once the last LDS exchange of codeword g is done, each wave streams positions r = 0, 1 of its share
+// of codeword g + gridDim.x into the (then idle) exchange buffer with global_load_lds (its own 8 KiB: 2 positions
+// x 4 x 1 KiB, lane-linear), behind the remaining FFT layers and the stores; the next codeword reads them from LDS
+// and loads only r = 2, 3 from HBM.
 template <int OM>  // the body of the waves with (W3, W2) = OM
 __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
-  const int lane = threadIdx.x & 63;
-  int wg = blockIdx.x;
-  const int slice = wg % a.slices;
-  wg /= a.slices;
-  const int cw = wg % a.cw_per_blk, blk = wg / a.cw_per_blk;
-  const int u = lane & 7;
-  const long long off = (long long)slice * 512 + u * 64;
-  const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
-  uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
-  uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
-  Ctx cx{a.cpoly, lane, w, {}};
+  const int lane0 = threadIdx.x & 63;
+  Ctx cx{a.cpoly, lane0, w, {}, ((lane0 >> 3) & 1) ? ~0u : 0u};
+  asm volatile("" : "+v"(cx.lm3));
   lv_fetch_all(cx);
-  uint32_t lm3 = ((lane >> 3) & 1) ? ~0u : 0u;
-  asm volatile("" : "+v"(lm3));
+  uint4* xw = xb + w * 512;  // this wave's prefetch slots [r = 0, 1][q = 0..3][lane]
+  bool pre = false;          // positions r = 0, 1 of codeword g are in xw
+  for (int g = blockIdx.x; g < a.total; g += gridDim.x) {
+    // opaque per iteration: otherwise LICM hoists the per-lane multiplies' 16 masks per constant (all derived from
+    // loop-invariant values) out of the loop and the register allocator spills
+#pragma unroll
+    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(cx.lv[i]));
+    asm volatile("" : "+v"(cx.lm3));
+    int lane = lane0;  // likewise for the lane-derived LDS exchange addresses
+    asm volatile("" : "+v"(lane));
+    const int u = lane & 7;
+    const int pl = pos_lane(LA, lane) + pos_wave(LA, w);
+    const SliceMasks km = slice_masks();
+    const int slice = g % a.slices;
+    const int cw = (g / a.slices) % a.cw_per_blk, blk = (g / a.slices) / a.cw_per_blk;
+    const long long off = (long long)slice * 512 + u * 64;
+    const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
+    uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
+    uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
 
-  uint32_t E[4][16];
-  const SliceMasks km = slice_masks();
-  const int pl = pos_lane(LA, lane) + pos_wave(LA, w);
+    uint32_t E[4][16];
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int s = pl + pos_r(LA, r);  // data shard s sits at point m + s (all k = m shards present)
-    const uint4* p = reinterpret_cast<const uint4*>(src + s * a.src_sh);
-    uint4 q0, q1, q2, q3;
-    if (a.mode < 2) {  // modes >= 2: synthetic data, no loads
-      q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    } else {
-      q0 = make_uint4(s, lane, w, r), q1 = make_uint4(lane * 3, s ^ 5, 7, w), q2 = q0, q3 = q1;
+    for (int r = 0; r < 4; r++) {
+      const int s = pl + pos_r(LA, r);  // data shard s sits at point m + s (all k = m shards present)
+      const uint4* p = reinterpret_cast<const uint4*>(src + s * a.src_sh);
+      uint4 q0, q1, q2, q3;
+      if (r < 2 && pre) {
+        q0 = xw[(r * 4 + 0) * 64 + lane], q1 = xw[(r * 4 + 1) * 64 + lane];
+        q2 = xw[(r * 4 + 2) * 64 + lane], q3 = xw[(r * 4 + 3) * 64 + lane];
+      } else if (a.mode < 2) {  // modes >= 2: synthetic data, no loads
+        q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+      } else {
+        q0 = make_uint4(s, lane, w, r), q1 = make_uint4(lane * 3, s ^ 5, 7, w), q2 = q0, q3 = q1;
+      }
+      if (cpy) {
+        uint4* o = reinterpret_cast<uint4*>(cpy + s * a.cpy_sh);
+        o[0] = q0;
+        o[1] = q1;
+        o[2] = q2;
+        o[3] = q3;
+      }
+      uint32_t lo[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+      uint32_t hi[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+      bitslice8(lo, km);
+      bitslice8(hi, km);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        E[r][j] = lo[j];
+        E[r][8 + j] = hi[j];
+      }
+      change_basis<false>(E[r]);
     }
-    if (cpy) {
-      uint4* o = reinterpret_cast<uint4*>(cpy + s * a.cpy_sh);
-      o[0] = q0;
-      o[1] = q1;
-      o[2] = q2;
-      o[3] = q3;
+    const int gn = g + (int)gridDim.x;
+    pre = false;
+    if (a.mode != 1) {
+      // IFFT, D = 1 .. m/2
+      layer<LA, true, 0, OM>(E, cx);
+      layer<LA, true, 1, OM>(E, cx);
+      swap_lane45(E);
+      layer<LB, true, 2, OM>(E, cx);
+      swap_lane3(E, cx.lm3);
+      layer<LC, true, 3, OM>(E, cx);
+      layer<LC, true, 4, OM>(E, cx);
+      __syncthreads();  // every wave has read its prefetch slots before the exchange overwrites them
+      exchange_w<0>(E, xb, w, lane);
+      layer<LD, true, 5, OM>(E, cx);
+      layer<LD, true, 6, OM>(E, cx);
+      exchange_w<1>(E, xb, w, lane);
+      layer<LE, true, 7, OM>(E, cx);
+      layer<LE, true, 8, OM>(E, cx);
+      // FFT, D = m/2 .. 1
+      layer<LE, false, 8, OM>(E, cx);
+      layer<LE, false, 7, OM>(E, cx);
+      exchange_w<1>(E, xb, w, lane);
+      layer<LD, false, 6, OM>(E, cx);
+      layer<LD, false, 5, OM>(E, cx);
+      exchange_w<0>(E, xb, w, lane);  // ends with a barrier: the exchange buffer is free until the next codeword
+      {  // issued unconditionally (no branch with the state live): without a next codeword, re-read this one
+        const int gp = gn < a.total ? gn : g;
+        const int sl = gp % a.slices;
+        const int cwn = (gp / a.slices) % a.cw_per_blk, bn = (gp / a.slices) / a.cw_per_blk;
+        const uint8_t* srcn = a.src + bn * a.src_blk + cwn * a.src_cw + (long long)sl * 512 + u * 64;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          const uint8_t* sp = srcn + (pl + pos_r(LA, r)) * a.src_sh;
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            __builtin_amdgcn_global_load_lds((glb_ptr)(sp + 16 * q), (lds_ptr)(xw + (r * 4 + q) * 64), 16, 0, 0);
+        }
+        pre = a.mode == 0;
+      }
+      layer<LC, false, 4, OM>(E, cx);
+      layer<LC, false, 3, OM>(E, cx);
+      swap_lane3(E, cx.lm3);
+      layer<LB, false, 2, OM>(E, cx);
+      swap_lane45(E);
+      layer<LA, false, 1, OM>(E, cx);
+      layer<LA, false, 0, OM>(E, cx);
     }
-    uint32_t lo[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-    uint32_t hi[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-    bitslice8(lo, km);
-    bitslice8(hi, km);
+    if (a.mode == 3) continue;
+    // parity shard s = point s
+    const SliceMasks ko = slice_masks();
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      E[r][j] = lo[j];
-      E[r][8 + j] = hi[j];
+    for (int r = 0; r < 4; r++) {
+      const int s = pl + pos_r(LA, r);
+      uint32_t v[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = E[r][j];
+      change_basis<true>(v);
+      uint32_t lo[8], hi[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        lo[j] = v[j];
+        hi[j] = v[8 + j];
+      }
+      bitslice8(lo, ko);
+      bitslice8(hi, ko);
+      uint4* o = reinterpret_cast<uint4*>(dst + s * a.dst_sh);
+      o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+      o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
+      o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+      o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
     }
-    change_basis<false>(E[r]);
-  }
-  if (a.mode == 1) goto store;
-  // IFFT, D = 1 .. m/2
-  layer<LA, true, 0, OM>(E, cx);
-  layer<LA, true, 1, OM>(E, cx);
-  swap_lane45(E);
-  layer<LB, true, 2, OM>(E, cx);
-  swap_lane3(E, lm3);
-  layer<LC, true, 3, OM>(E, cx);
-  layer<LC, true, 4, OM>(E, cx);
-  exchange_w<0>(E, xb, w, lane);
-  layer<LD, true, 5, OM>(E, cx);
-  layer<LD, true, 6, OM>(E, cx);
-  exchange_w<1>(E, xb, w, lane);
-  layer<LE, true, 7, OM>(E, cx);
-  layer<LE, true, 8, OM>(E, cx);
-  // FFT, D = m/2 .. 1
-  layer<LE, false, 8, OM>(E, cx);
-  layer<LE, false, 7, OM>(E, cx);
-  exchange_w<1>(E, xb, w, lane);
-  layer<LD, false, 6, OM>(E, cx);
-  layer<LD, false, 5, OM>(E, cx);
-  exchange_w<0>(E, xb, w, lane);
-  layer<LC, false, 4, OM>(E, cx);
-  layer<LC, false, 3, OM>(E, cx);
-  swap_lane3(E, lm3);
-  layer<LB, false, 2, OM>(E, cx);
-  swap_lane45(E);
-  layer<LA, false, 1, OM>(E, cx);
-  layer<LA, false, 0, OM>(E, cx);
-store:
-  if (a.mode == 3 && blockIdx.x != 0x7FFFFFFF) return;
-  // parity shard s = point s
-  const SliceMasks ko = slice_masks();
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int s = pl + pos_r(LA, r);
-    uint32_t v[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = E[r][j];
-    change_basis<true>(v);
-    uint32_t lo[8], hi[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      lo[j] = v[j];
-      hi[j] = v[8 + j];
-    }
-    bitslice8(lo, ko);
-    bitslice8(hi, ko);
-    uint4* o = reinterpret_cast<uint4*>(dst + s * a.dst_sh);
-    o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-    o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
-    o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-    o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
   }
 }
 
@@ -534,8 +592,17 @@ int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t 
     return e ? atoi(e) : 0;
   }();
   a.mode = mode;
-  const long long grid = (long long)j.nblk * j.cw_per_blk * a.slices;
-  if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
+  const long long total = (long long)j.nblk * j.cw_per_blk * a.slices;
+  if (total <= 0 || total > 0x7FFFFFFF) return -2;
+  a.total = (int)total;
+  static const int ncu = [] {  // one persistent workgroup per CU
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int grid = (int)(total < ncu ? total : ncu);
   hipLaunchKernelGGL(r16::rs_encode16_reg_kernel, dim3((unsigned)grid), dim3(1024), 128 * 1024, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
