@@ -390,6 +390,44 @@ struct Args {
   int mode;  // diagnostics (CDA_RS16_MODE): 0 = encode; 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores
 };
 
+// Coalesced shard access.  Leopard's GF(2^16) shard layout pairs element e of each 64-B block with bytes e (low)
+// and 32 + e (high).  Lane u (= lane & 7) of a position moves the 16-B chunks at u*16 + 128q, q = 0..3, so the 8
+// lanes of a position cover 128 contiguous bytes per instruction (64-B strided chunks cost 4x the memory requests):
+// lanes with lane bit 1 clear hold low halves, their partners (lane ^ 2, one DPP quad_perm) the matching high
+// halves.  pair_in trades chunks so that each lane holds low + high bytes of 32 whole elements (blocks 2q + (u>>2)
+// for q = 0, 1 on the low lane, q = 2, 3 on the high lane); pair_out is its inverse.  m1 = all-ones iff lane bit 1.
+__device__ __forceinline__ uint32_t xq2(uint32_t v) {  // v of lane ^ 2
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+}
+__device__ __forceinline__ void pair_in(const uint4& q0, const uint4& q1, const uint4& q2, const uint4& q3, uint32_t m1,
+                                        uint32_t (&lo)[8], uint32_t (&hi)[8]) {
+  const uint32_t a[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  const uint32_t b[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t rv = xq2(sel(m1, a[i], b[i]));  // low lane sends b, high lane sends a
+    lo[i] = sel(m1, rv, a[i]);
+    hi[i] = sel(m1, b[i], rv);
+  }
+}
+__device__ __forceinline__ void pair_out(const uint32_t (&lo)[8], const uint32_t (&hi)[8], uint32_t m1, uint4& q0,
+                                         uint4& q1, uint4& q2, uint4& q3) {
+  uint32_t a[8], b[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t rv = xq2(sel(m1, lo[i], hi[i]));  // low lane sends hi, high lane sends lo
+    a[i] = sel(m1, rv, lo[i]);
+    b[i] = sel(m1, hi[i], rv);
+  }
+  q0 = make_uint4(a[0], a[1], a[2], a[3]);
+  q1 = make_uint4(a[4], a[5], a[6], a[7]);
+  q2 = make_uint4(b[0], b[1], b[2], b[3]);
+  q3 = make_uint4(b[4], b[5], b[6], b[7]);
+}
+
 typedef __attribute__((address_space(1))) void* glb_ptr;
 typedef __attribute__((address_space(3))) void* lds_ptr;
 
@@ -418,9 +456,11 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
     const int u = lane & 7;
     const int pl = pos_lane(LA, lane) + pos_wave(LA, w);
     const SliceMasks km = slice_masks();
+    uint32_t m1 = (lane & 2) ? ~0u : 0u;
+    asm volatile("" : "+v"(m1));
     const int slice = g % a.slices;
     const int cw = (g / a.slices) % a.cw_per_blk, blk = (g / a.slices) / a.cw_per_blk;
-    const long long off = (long long)slice * 512 + u * 64;
+    const long long off = (long long)slice * 512 + u * 16;
     const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
     uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
     uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
@@ -435,19 +475,19 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
         q0 = xw[(r * 4 + 0) * 64 + lane], q1 = xw[(r * 4 + 1) * 64 + lane];
         q2 = xw[(r * 4 + 2) * 64 + lane], q3 = xw[(r * 4 + 3) * 64 + lane];
       } else if (a.mode < 2) {  // modes >= 2: synthetic data, no loads
-        q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+        q0 = p[0], q1 = p[8], q2 = p[16], q3 = p[24];
       } else {
         q0 = make_uint4(s, lane, w, r), q1 = make_uint4(lane * 3, s ^ 5, 7, w), q2 = q0, q3 = q1;
       }
       if (cpy) {
         uint4* o = reinterpret_cast<uint4*>(cpy + s * a.cpy_sh);
         o[0] = q0;
-        o[1] = q1;
-        o[2] = q2;
-        o[3] = q3;
+        o[8] = q1;
+        o[16] = q2;
+        o[24] = q3;
       }
-      uint32_t lo[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-      uint32_t hi[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+      uint32_t lo[8], hi[8];
+      pair_in(q0, q1, q2, q3, m1, lo, hi);
       bitslice8(lo, km);
       bitslice8(hi, km);
 #pragma unroll
@@ -486,13 +526,13 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
         const int gp = gn < a.total ? gn : g;
         const int sl = gp % a.slices;
         const int cwn = (gp / a.slices) % a.cw_per_blk, bn = (gp / a.slices) / a.cw_per_blk;
-        const uint8_t* srcn = a.src + bn * a.src_blk + cwn * a.src_cw + (long long)sl * 512 + u * 64;
+        const uint8_t* srcn = a.src + bn * a.src_blk + cwn * a.src_cw + (long long)sl * 512 + u * 16;
 #pragma unroll
         for (int r = 0; r < 2; r++) {
           const uint8_t* sp = srcn + (pl + pos_r(LA, r)) * a.src_sh;
 #pragma unroll
           for (int q = 0; q < 4; q++)
-            __builtin_amdgcn_global_load_lds((glb_ptr)(sp + 16 * q), (lds_ptr)(xw + (r * 4 + q) * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr)(sp + 128 * q), (lds_ptr)(xw + (r * 4 + q) * 64), 16, 0, 0);
         }
         pre = a.mode == 0;
       }
@@ -523,10 +563,12 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
       bitslice8(lo, ko);
       bitslice8(hi, ko);
       uint4* o = reinterpret_cast<uint4*>(dst + s * a.dst_sh);
-      o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-      o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
-      o[2] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-      o[3] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+      uint4 q0, q1, q2, q3;
+      pair_out(lo, hi, m1, q0, q1, q2, q3);
+      o[0] = q0;
+      o[8] = q1;
+      o[16] = q2;
+      o[24] = q3;
     }
   }
 }
