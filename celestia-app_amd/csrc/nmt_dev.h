@@ -245,32 +245,41 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
   for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
 }
 
+// Message block B (0..2) of an inner node: 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits), children in
+// record layout (24 words each).
+template <int B>
+__device__ __forceinline__ void node_block(const uint32_t (&L)[24], const uint32_t (&R)[24], uint32_t (&m)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int wi = 16 * B + i;
+    if (wi == 0) m[i] = be_window(0x01000000u, L[0], 3);
+    else if (wi <= 21) m[i] = be_window(L[wi - 1], L[wi], 3);
+    else if (wi == 22) m[i] = be_window(L[21], L[22], 3) | (R[0] & 0xFFu);
+    else if (wi <= 44) m[i] = be_window(R[wi - 23], R[wi - 22], 1);
+    else if (wi == 45) m[i] = be_window(R[22], R[23], 1) | 0x00800000u;
+    else if (wi == 46) m[i] = 0;
+    else m[i] = 181u * 8u;
+  }
+}
+// The node record from its children and the digest state: min = L.min; max = R.min == parity ns ? L.max : R.max.
+__device__ __forceinline__ void node_record(const uint32_t (&L)[24], const uint32_t (&R)[24], const uint32_t (&st)[8],
+                                            uint32_t (&o)[24]);
+
 // hash_node_mem with both children already in registers (24 words each, record layout): the form for latency
 // kernels that run one wave per SIMD, where registers are free and a memory round trip per compression is not.
 __device__ __forceinline__ void hash_node_regs(const uint32_t (&L)[24], const uint32_t (&R)[24], uint32_t (&o)[24]) {
   uint32_t st[8], m[16];
   sha256_init(st);
-  m[0] = be_window(0x01000000u, L[0], 3);
-#pragma unroll
-  for (int i = 1; i < 16; i++) m[i] = be_window(L[i - 1], L[i], 3);
+  node_block<0>(L, R, m);
   sha256_compress(st, m);
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int wi = 16 + i;
-    if (wi <= 21) m[i] = be_window(L[wi - 1], L[wi], 3);
-    else if (wi == 22) m[i] = be_window(L[21], L[22], 3) | (R[0] & 0xFFu);
-    else m[i] = be_window(R[wi - 23], R[wi - 22], 1);
-  }
+  node_block<1>(L, R, m);
   sha256_compress(st, m);
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int wi = 32 + i;
-    if (wi <= 44) m[i] = be_window(R[wi - 23], R[wi - 22], 1);
-    else if (wi == 45) m[i] = be_window(R[22], R[23], 1) | 0x00800000u;
-    else if (wi == 46) m[i] = 0;
-    else m[i] = 181u * 8u;
-  }
+  node_block<2>(L, R, m);
   sha256_compress(st, m);
+  node_record(L, R, st, o);
+}
+__device__ __forceinline__ void node_record(const uint32_t (&L)[24], const uint32_t (&R)[24], const uint32_t (&st)[8],
+                                            uint32_t (&o)[24]) {
   bool rmin_max = true;
 #pragma unroll
   for (int i = 0; i < 7; i++) rmin_max &= (R[i] == 0xFFFFFFFFu);

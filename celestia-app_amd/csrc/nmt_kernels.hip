@@ -187,24 +187,44 @@ int launch_nmt_trees(const void* d_leaves, void* d_levels, void* d_roots, int k,
 // Levels pair (2i, 2i+1) and promote an odd last node, which is the same tree as
 // HashFromByteSlices' "split at the largest power of two below n" recursion.
 // ---------------------------------------------------------------------------
-// DAH leaf digest: SHA256(0x00 || root record[0..90)) as 8 big-endian words
-__device__ __forceinline__ void dah_leaf_digest(const uint32_t (&L)[24], uint32_t (&st)[8]) {
-  uint32_t m[16];
-  sha256_init(st);
+// DAH leaf digest: SHA256(0x00 || root record[0..90)) as 8 big-endian words; message block B of it
+template <int B>
+__device__ __forceinline__ void dah_leaf_block(const uint32_t (&L)[24], uint32_t (&m)[16]) {
   // 0x00 ‖ root[0..90) ‖ 0x80 ‖ ... ‖ len(91*8)
-  m[0] = be_window(0u, L[0], 3);
-#pragma unroll
-  for (int t = 1; t < 16; t++) m[t] = be_window(L[t - 1], L[t], 3);
-  sha256_compress(st, m);
 #pragma unroll
   for (int t = 0; t < 16; t++) {
-    const int wi = 16 + t;
-    if (wi <= 21) m[t] = be_window(L[wi - 1], L[wi], 3);
+    const int wi = 16 * B + t;
+    if (wi == 0) m[t] = be_window(0u, L[0], 3);
+    else if (wi <= 21) m[t] = be_window(L[wi - 1], L[wi], 3);
     else if (wi == 22) m[t] = be_window(L[21], L[22], 3) | 0x80u;
     else if (wi < 31) m[t] = 0;
     else m[t] = 91u * 8u;
   }
+}
+__device__ __forceinline__ void dah_leaf_digest(const uint32_t (&L)[24], uint32_t (&st)[8]) {
+  uint32_t m[16];
+  sha256_init(st);
+  dah_leaf_block<0>(L, m);
   sha256_compress(st, m);
+  dah_leaf_block<1>(L, m);
+  sha256_compress(st, m);
+}
+// RFC-6962 inner node message block B of digests Ld, Rd (8 big-endian words each): 0x01 ‖ Ld ‖ Rd ‖ pad, 65 bytes
+template <int B>
+__device__ __forceinline__ void rfc_node_block(const uint32_t* Ld, const uint32_t* Rd, uint32_t (&m)[16]) {
+  if (B == 0) {
+    m[0] = 0x01000000u | (Ld[0] >> 8);
+#pragma unroll
+    for (int t = 1; t < 8; t++) m[t] = (Ld[t - 1] << 24) | (Ld[t] >> 8);
+    m[8] = (Ld[7] << 24) | (Rd[0] >> 8);
+#pragma unroll
+    for (int t = 9; t < 16; t++) m[t] = (Rd[t - 9] << 24) | (Rd[t - 8] >> 8);
+  } else {
+    m[0] = (Rd[7] << 24) | 0x00800000u;
+#pragma unroll
+    for (int t = 1; t < 15; t++) m[t] = 0;
+    m[15] = 65u * 8u;
+  }
 }
 
 // RFC-6962 levels over the n leaf digests at sdig ([n + (n+1)/2][8] words of LDS, the first n filled), by the
@@ -226,20 +246,75 @@ __device__ __forceinline__ void dah_fold(uint32_t* sdig, int n, uint32_t* out) {
       const uint32_t* Rd = src + (2 * i + 1) * 8;
       uint32_t st[8], m[16];
       sha256_init(st);
-      m[0] = 0x01000000u | (Ld[0] >> 8);
-#pragma unroll
-      for (int t = 1; t < 8; t++) m[t] = (Ld[t - 1] << 24) | (Ld[t] >> 8);
-      m[8] = (Ld[7] << 24) | (Rd[0] >> 8);
-#pragma unroll
-      for (int t = 9; t < 16; t++) m[t] = (Rd[t - 9] << 24) | (Rd[t - 8] >> 8);
+      rfc_node_block<0>(Ld, Rd, m);
       sha256_compress(st, m);
-      m[0] = (Rd[7] << 24) | 0x00800000u;
-#pragma unroll
-      for (int t = 1; t < 15; t++) m[t] = 0;
-      m[15] = 65u * 8u;
+      rfc_node_block<1>(Ld, Rd, m);
       sha256_compress(st, m);
 #pragma unroll
       for (int t = 0; t < 8; t++) o[t] = st[t];
+    }
+    __syncthreads();
+    uint32_t* tmp = src;
+    src = dst;
+    dst = tmp;
+    cnt = out_cnt;
+  }
+  if (threadIdx.x < 8) out[threadIdx.x] = bswap(src[threadIdx.x]);
+}
+
+// dah_fold for the latency path (trees_lds_kernel's last workgroup, >= 128 threads): once a level has at most 64
+// nodes, wave 0 hashes them while wave 1 expands each node's second message block into kw (64 x kKwStride words of
+// LDS), and the second compression then runs its rounds alone.
+__device__ __forceinline__ void dah_fold_kw(uint32_t* sdig, int n, uint32_t* out, uint32_t* kw) {
+  uint32_t* src = sdig;
+  uint32_t* dst = sdig + n * 8;
+  for (int cnt = n; cnt > 1;) {
+    const int out_cnt = (cnt + 1) >> 1;
+    if (out_cnt > 64) {
+      for (int i = threadIdx.x; i < out_cnt; i += blockDim.x) {
+        uint32_t* o = dst + i * 8;
+        const uint32_t* Ld = src + (2 * i) * 8;
+        if (2 * i + 1 >= cnt) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) o[t] = Ld[t];
+          continue;
+        }
+        const uint32_t* Rd = src + (2 * i + 1) * 8;
+        uint32_t st[8], m[16];
+        sha256_init(st);
+        rfc_node_block<0>(Ld, Rd, m);
+        sha256_compress(st, m);
+        rfc_node_block<1>(Ld, Rd, m);
+        sha256_compress(st, m);
+#pragma unroll
+        for (int t = 0; t < 8; t++) o[t] = st[t];
+      }
+    } else {
+      const int i = threadIdx.x & 63;
+      const bool pair = i < out_cnt && 2 * i + 1 < cnt;
+      uint32_t st[8];
+      if (threadIdx.x < 64 && i < out_cnt) {
+        const uint32_t* Ld = src + (2 * i) * 8;
+        if (pair) {
+          uint32_t m[16];
+          sha256_init(st);
+          rfc_node_block<0>(Ld, src + (2 * i + 1) * 8, m);
+          sha256_compress(st, m);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; t++) dst[i * 8 + t] = Ld[t];
+        }
+      } else if (threadIdx.x >= 64 && threadIdx.x < 128 && pair) {
+        uint32_t m[16];
+        rfc_node_block<1>(src + (2 * i) * 8, src + (2 * i + 1) * 8, m);
+        sha256_kw_store(m, kw + i * kKwStride);
+      }
+      __syncthreads();
+      if (threadIdx.x < 64 && pair) {
+        sha256_rounds_kw(st, kw + i * kKwStride);
+#pragma unroll
+        for (int t = 0; t < 8; t++) dst[i * 8 + t] = st[t];
+      }
     }
     __syncthreads();
     uint32_t* tmp = src;
@@ -276,6 +351,14 @@ __global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ root
 // put back to 0 for the next call) folds the block's digests into the DAH, so the step needs no DAH launch.  The
 // batched form (nmt_levels_kernel + dah_kernel) keeps every lane on a useful node and stays the throughput path.
 constexpr int kLdsRec = 7;  // uint4 per LDS record
+__device__ __forceinline__ void load_pair(const uint4* in, int i, uint32_t (&L)[24], uint32_t (&R)[24]) {
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    const uint4 u = in[(2 * i) * kLdsRec + q], v = in[(2 * i + 1) * kLdsRec + q];
+    L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
+    R[4 * q] = v.x, R[4 * q + 1] = v.y, R[4 * q + 2] = v.z, R[4 * q + 3] = v.w;
+  }
+}
 __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict__ leaves, uint4* __restrict__ roots,
                                                         uint32_t* __restrict__ dah, unsigned* __restrict__ done,
                                                         uint32_t* __restrict__ digests, int log2w) {
@@ -291,6 +374,8 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   if (threadIdx.x == 0) last = 0;  // published by the barrier after the leaf copy
   uint4* A = lds + (size_t)half * (w + w / 2) * kLdsRec;
   uint4* B = A + (size_t)w * kLdsRec;
+  // K+W schedules of blocks 1 and 2 of up to 64 nodes per tree, after both halves' records
+  uint32_t* kw = reinterpret_cast<uint32_t*>(lds + (size_t)2 * (w + w / 2 + 1) * kLdsRec) + half * 2 * 64 * kKwStride;
   for (int x = ht; x < w * 6; x += 128) {  // 16-B words of the w records, adjacent lanes adjacent
     const int i = x / 6, q = x - i * 6;
     const size_t rec = col ? ((size_t)i << log2w) + t : ((size_t)t << log2w) + i;
@@ -300,34 +385,72 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   for (int l = 1; l <= log2w; l++) {
     const uint4* in = (l & 1) ? A : B;
     uint4* out = (l & 1) ? B : A;
-    for (int i = ht; i < (w >> l); i += 128) {
-      uint32_t L[24], R[24], o[24];
+    const int nodes = w >> l;
+    if (nodes > 64) {
+      for (int i = ht; i < nodes; i += 128) {
+        uint32_t L[24], R[24], o[24];
+        load_pair(in, i, L, R);
+        hash_node_regs(L, R, o);
 #pragma unroll
-      for (int q = 0; q < 6; q++) {
-        const uint4 u = in[(2 * i) * kLdsRec + q], v = in[(2 * i + 1) * kLdsRec + q];
-        L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
-        R[4 * q] = v.x, R[4 * q + 1] = v.y, R[4 * q + 2] = v.z, R[4 * q + 3] = v.w;
+        for (int q = 0; q < 6; q++) out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
       }
-      hash_node_regs(L, R, o);
+    } else {
+      // wave 0 of the half hashes block 0 of node ht while wave 1 expands blocks 1 and 2 of node ht - 64; after
+      // the barrier wave 0 runs the last two compressions from the precomputed schedules
+      const int i = ht & 63;
+      uint32_t L[24], R[24], st[8];
+      if (i < nodes) load_pair(in, i, L, R);
+      if (ht < 64 && i < nodes) {
+        uint32_t m[16];
+        sha256_init(st);
+        node_block<0>(L, R, m);
+        sha256_compress(st, m);
+      } else if (ht >= 64 && i < nodes) {
+        uint32_t m[16];
+        node_block<1>(L, R, m);
+        sha256_kw_store(m, kw + i * kKwStride);
+        node_block<2>(L, R, m);
+        sha256_kw_store(m, kw + (64 + i) * kKwStride);
+      }
+      __syncthreads();
+      if (ht < 64 && i < nodes) {
+        sha256_rounds_kw(st, kw + i * kKwStride);
+        sha256_rounds_kw(st, kw + (64 + i) * kKwStride);
+        uint32_t o[24];
+        node_record(L, R, st, o);
 #pragma unroll
-      for (int q = 0; q < 6; q++) out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        for (int q = 0; q < 6; q++) out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+      }
     }
     __syncthreads();
   }
   const uint4* root = (log2w & 1) ? B : A;
   uint4* rout = roots + ((size_t)b * n + tree) * 6;
   if (ht < 6) rout[ht] = root[ht];
-  if (ht == 0) {  // this root's DAH leaf digest
-    uint32_t L[24], st[8];
+  {  // this root's DAH leaf digest: block 0 by lane 0, block 1's schedule by lane 64 meanwhile
+    uint32_t L[24], st[8], m[16];
+    if (ht == 0 || ht == 64) {
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-      const uint4 u = root[q];
-      L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
+      for (int q = 0; q < 6; q++) {
+        const uint4 u = root[q];
+        L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
+      }
     }
-    dah_leaf_digest(L, st);
-    uint4* dg = reinterpret_cast<uint4*>(digests + ((size_t)b * n + tree) * 8);
-    dg[0] = make_uint4(st[0], st[1], st[2], st[3]);
-    dg[1] = make_uint4(st[4], st[5], st[6], st[7]);
+    if (ht == 0) {
+      sha256_init(st);
+      dah_leaf_block<0>(L, m);
+      sha256_compress(st, m);
+    } else if (ht == 64) {
+      dah_leaf_block<1>(L, m);
+      sha256_kw_store(m, kw);
+    }
+    __syncthreads();
+    if (ht == 0) {
+      sha256_rounds_kw(st, kw);
+      uint4* dg = reinterpret_cast<uint4*>(digests + ((size_t)b * n + tree) * 8);
+      dg[0] = make_uint4(st[0], st[1], st[2], st[3]);
+      dg[1] = make_uint4(st[4], st[5], st[6], st[7]);
+    }
   }
   __syncthreads();  // both halves' roots and digests are stored (each by lanes of the wave that increments below)
   if (threadIdx.x == 0 || threadIdx.x == 128) {  // one increment per tree, from the wave that stored it
@@ -341,7 +464,7 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   const uint4* src = reinterpret_cast<const uint4*>(digests + (size_t)b * n * 8);
   for (int x = threadIdx.x; x < n * 2; x += blockDim.x) reinterpret_cast<uint4*>(sdig)[x] = src[x];
   __syncthreads();
-  dah_fold(sdig, n, dah + b * 8);
+  dah_fold_kw(sdig, n, dah + b * 8, sdig + (n + (n + 1) / 2) * 8);
   if (threadIdx.x == 0) __hip_atomic_store(done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -456,8 +579,10 @@ int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned*
   while ((1 << log2w) < w) log2w++;
   if ((1 << log2w) != w || log2w < 1) return -2;
   if (w > 256) return -2;  // a thread per node of level 1 within a 128-thread half
-  // two trees x (w + w / 2) records of 112 B; >= (2w + w) x 32 B of DAH digests
-  const size_t lds = 2 * ((size_t)w + w / 2 + 1) * kLdsRec * 16;
+  // two trees x (w + w / 2) records of 112 B, then 2 x 2 x 64 schedule rows of kKwStride words; the DAH fold
+  // reuses it: (2w + w) x 32 B of digests + 64 schedule rows
+  const size_t lds = 2 * ((size_t)w + w / 2 + 1) * kLdsRec * 16 + (size_t)4 * 64 * kKwStride * 4;
+  if ((size_t)(2 * w + w) * 32 + (size_t)64 * kKwStride * 4 > lds) return -2;
   // the dynamic-LDS limit is raised to what the launch needs: 160 KiB would exceed the CU's LDS by the kernel's
   // static __shared__ word and the call would fail (and with it the launch)
   if (lds > 64 * 1024 &&

@@ -101,6 +101,64 @@ __device__ __forceinline__ void sha256_compress(uint32_t s[8], uint32_t w[16]) {
   s[7] += h;
 }
 
+// Latency path (one wave per SIMD, where a lone wave issues about one instruction per 5.4 cycles whatever its
+// ILP, so a compression costs its instruction count): a block's message schedule does not depend on the chaining
+// state, so an otherwise idle wave can expand it beforehand.  sha256_kw_store writes kw[t] = K[t] + W[t] for the
+// 64 rounds (one LDS row of kKwStride words: node-major, 4-word writes / reads are bank-conflict free over 16
+// lanes); sha256_rounds_kw then runs the 64 rounds alone: about 900 instructions instead of 1,440.
+constexpr int kKwStride = 68;
+__device__ __forceinline__ void sha256_kw_store(uint32_t (&w)[16], uint32_t* kw) {
+#pragma unroll
+  for (int t4 = 0; t4 < 16; t4++) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int t = 4 * t4 + j;
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+        const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        w[t & 15] = wt;
+      }
+      v[j] = wt + K256::v[t];
+    }
+    reinterpret_cast<uint4*>(kw)[t4] = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+__device__ __forceinline__ void sha256_rounds_kw(uint32_t s[8], const uint32_t* kw) {
+  uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+  for (int t4 = 0; t4 < 16; t4++) {
+    const uint4 q = reinterpret_cast<const uint4*>(kw)[t4];
+    const uint32_t kv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + kv[j];
+      const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
+      h = g;
+      g = f;
+      f = e;
+      e = d + t1;
+      d = c;
+      c = b;
+      b = a;
+      a = t1 + t2;
+    }
+  }
+  s[0] += a;
+  s[1] += b;
+  s[2] += c;
+  s[3] += d;
+  s[4] += e;
+  s[5] += f;
+  s[6] += g;
+  s[7] += h;
+}
+
 // N independent compressions advanced in lockstep (round-interleaved), giving
 // the scheduler N independent dependency chains per wave.
 template <int N, int SB = 0>
