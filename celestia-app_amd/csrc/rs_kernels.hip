@@ -461,6 +461,7 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
     }
   }
   constexpr int F2 = L - 3;  // P2 register bits F2..F2+2 = L-3..L-1
+#ifndef CDA_RS8_DIAG_NOCOMPUTE  // diagnostic build (scripts/rs8_diag.sh): loads and stores only
   // P1 (f=1): IFFT d=0 (cross-lane), d=1..3 (or up to L-1 when L == 4)
   p1_w<L, WC>(E, lm);
   if (L > 4) exchange2<M>(E, xbuf, WC, sw, li, 1, F2);
@@ -469,6 +470,10 @@ __device__ __forceinline__ void rs_g2_impl(const Rs8RegArgs& a, int wg, uint4* x
   if (L > 4) exchange2<M>(E, xbuf, WC, sw, li, F2, 1);
   // P3 (f=1): FFT d=F2-1..1, then d=0 (cross-lane)
   p3_w<L, WC>(E, lm);
+#else
+  (void)lm;
+  (void)F2;
+#endif
   const SliceMasks ko = slice_masks();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
