@@ -180,6 +180,7 @@ struct Rs8RegArgs {
   uint8_t* cpy;
   long long cpy_blk, cpy_cw, cpy_sh;
   int k, groups_per_blk, slices;
+  int remap;  // XCD-contiguous workgroup order
 };
 
 // ===========================================================================
@@ -512,7 +513,11 @@ __device__ __forceinline__ void rs_g2_body(const Rs8RegArgs& a, int wg, uint4* x
 template <int L>
 __global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
-  rs_g2_body<L>(a, blockIdx.x, xbuf);
+  // XCD-contiguous work (a.remap): the dispatcher deals workgroups to the 8 XCDs round-robin, so XCD x runs blocks
+  // x, x + 8, ...; map them to one contiguous range of codeword pairs per XCD
+  const unsigned g = gridDim.x, b = blockIdx.x;
+  const int wg = (a.remap && (g % 8u) == 0) ? (int)((b % 8u) * (g / 8u) + b / 8u) : (int)b;
+  rs_g2_body<L>(a, wg, xbuf);
 }
 
 static Rs8RegArgs reg_args(const RsJob& j);
@@ -573,6 +578,9 @@ static Rs8RegArgs reg_args(const RsJob& j) {
   r.k = j.k;
   r.groups_per_blk = j.cw_per_blk / 2;
   r.slices = j.shard_len / 512;
+  // XCD-contiguous order for the row pass only (positions contiguous): rows 0.599 -> 0.580 ms per B = 128 step; the
+  // column pass got slower with it (0.826 -> 0.877 ms), scripts/env_ab_bench.sh, round 3
+  r.remap = j.src_sh == j.shard_len;
   return r;
 }
 
