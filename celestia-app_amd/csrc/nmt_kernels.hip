@@ -228,43 +228,11 @@ __device__ __forceinline__ void rfc_node_block(const uint32_t* Ld, const uint32_
 }
 
 // RFC-6962 levels over the n leaf digests at sdig ([n + (n+1)/2][8] words of LDS, the first n filled), by the
-// calling workgroup; the 32-B hash goes to out.  Levels pair (2i, 2i+1) and promote an odd last node, which is the
-// same tree as HashFromByteSlices' "split at the largest power of two below n" recursion.
-__device__ __forceinline__ void dah_fold(uint32_t* sdig, int n, uint32_t* out) {
-  uint32_t* src = sdig;
-  uint32_t* dst = sdig + n * 8;
-  for (int cnt = n; cnt > 1;) {
-    const int out_cnt = (cnt + 1) >> 1;
-    for (int i = threadIdx.x; i < out_cnt; i += blockDim.x) {
-      uint32_t* o = dst + i * 8;
-      const uint32_t* Ld = src + (2 * i) * 8;
-      if (2 * i + 1 >= cnt) {
-#pragma unroll
-        for (int t = 0; t < 8; t++) o[t] = Ld[t];
-        continue;
-      }
-      const uint32_t* Rd = src + (2 * i + 1) * 8;
-      uint32_t st[8], m[16];
-      sha256_init(st);
-      rfc_node_block<0>(Ld, Rd, m);
-      sha256_compress(st, m);
-      rfc_node_block<1>(Ld, Rd, m);
-      sha256_compress(st, m);
-#pragma unroll
-      for (int t = 0; t < 8; t++) o[t] = st[t];
-    }
-    __syncthreads();
-    uint32_t* tmp = src;
-    src = dst;
-    dst = tmp;
-    cnt = out_cnt;
-  }
-  if (threadIdx.x < 8) out[threadIdx.x] = bswap(src[threadIdx.x]);
-}
-
-// dah_fold for the latency path (trees_lds_kernel's last workgroup, >= 128 threads): once a level has at most 64
-// nodes, wave 0 hashes them while wave 1 expands each node's second message block into kw (64 x kKwStride words of
-// LDS), and the second compression then runs its rounds alone.
+// calling workgroup (>= 128 threads); the 32-B hash goes to out.  Levels pair (2i, 2i+1) and promote an odd last
+// node, which is the same tree as HashFromByteSlices' "split at the largest power of two below n" recursion.  Once
+// a level has at most 64 nodes (its chain of dependent compressions is the latency), wave 0 hashes block 0 of each
+// node while wave 1 expands the node's second message block into kw (64 x kKwStride words of LDS), and the second
+// compression then runs its rounds alone.
 __device__ __forceinline__ void dah_fold_kw(uint32_t* sdig, int n, uint32_t* out, uint32_t* kw) {
   uint32_t* src = sdig;
   uint32_t* dst = sdig + n * 8;
@@ -338,7 +306,7 @@ __global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ root
     for (int t = 0; t < 8; t++) sdig[i * 8 + t] = st[t];
   }
   __syncthreads();
-  dah_fold(sdig, n, dah + blockIdx.x * 8);
+  dah_fold_kw(sdig, n, dah + blockIdx.x * 8, sdig + (n + (n + 1) / 2) * 8);
 }
 
 // Small batches (the single block of ProcessProposal, config C2): every tree of the batch in ONE launch.  A
@@ -596,7 +564,8 @@ int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned*
 
 int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s) {
   if (n_roots_total < 1) return -2;
-  const size_t lds = ((size_t)n_roots_total + (n_roots_total + 1) / 2) * 32;
+  // digests, then 64 K+W schedule rows for dah_fold_kw
+  const size_t lds = ((size_t)n_roots_total + (n_roots_total + 1) / 2) * 32 + (size_t)64 * kKwStride * 4;
   if (lds > 160 * 1024) return -2;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute((const void*)dah_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
