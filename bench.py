@@ -446,6 +446,18 @@ def k512_measure(ctx, dev, reps=3):
            "path_hbm_gbs": round(block_bytes(k) * B / el / 1e9, 1),
            "kernels_ms": {n: round(ms / max(1, cnt), 3) for n, (ms, cnt) in prof.items()},
            "parity": "GF(2^16) unpinned by reference data (Lagrange-oracle checked)"}
+    # the same path with ONE square per call: the per-call fixed costs (the DAH's dependent chain, launch gaps) that
+    # two squares per call share -- the like-for-like reference for the split entry below (one square per call)
+    def step1():
+        ctx.extend_commit_device(k, 1, ods.data_ptr(), eds.data_ptr(), roots.data_ptr(), dah.data_ptr(),
+                                 st.data_ptr(), stream.cuda_stream)
+    step1()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step1()
+    torch.cuda.synchronize(dev)
+    out["one_square_per_call_ms"] = round((time.perf_counter() - t0) * 1e3 / reps, 3)
     del eds, roots
     # config C5's split path behind the C ABI (cda_multi_extend_commit_split_device): one square over the devices of
     # a handle.  On one GPU: G = 1 (the row slab is the column slab's top half, no exchange) and G = 8 replicas on
