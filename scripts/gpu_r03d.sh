@@ -3,7 +3,7 @@
 # bench line.  Each GPU step has its own time limit; stop at the first crash/timeout.
 set -u
 mkdir -p gpurun_out
-PROFILE=1 ./scripts/gpu_round.sh r03_v3 || exit $?
+PROFILE=1 ./scripts/gpu_round.sh ${TAG:-r03_v4} || exit $?
 echo "== c2"; timeout -k 10 120 python -u scripts/c2_probe.py > gpurun_out/c2_final.log 2>&1 || exit $?
 tail -c 600 gpurun_out/c2_final.log
 echo "== rs16"; timeout -k 10 120 python -u scripts/rs16_probe.py 20 > gpurun_out/rs16_final.log 2>&1 || exit $?
