@@ -64,6 +64,9 @@ int launch_nmt_level(const void* d_in, void* d_out, bool from_leaves, int k, int
 int launch_nmt_trees(const void* d_leaves, void* d_levels, void* d_roots, int k, int nblocks, hipStream_t s,
                      void* prof_ctx);
 int launch_dah(const void* d_roots, void* d_dah, int n_roots_total, int nblocks, hipStream_t s);
+// the batched path's DAH: digests by ceil(n / 256) workgroups per block, fold by the last (counters in d_done)
+int launch_dah_wide(const void* d_roots, void* d_dah, unsigned* d_done, void* d_digests, int n, int nblocks,
+                    hipStream_t s);
 // every tree of nblocks blocks in one launch (LDS-resident), the DAH by the last workgroup of each block;
 // d_done: nblocks zeroed counters (left zeroed); d_digests: nblocks x 4k x 32 B scratch
 int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned* d_done, void* d_digests, int k,

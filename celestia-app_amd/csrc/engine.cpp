@@ -228,9 +228,23 @@ int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void*
                                    (uint8_t*)c->scratch.p + 2 * rec_off * CDA_REC_BYTES, d_roots, (int)k, (int)nblocks, s,
                                    c);
   if (lr0) return lr0 == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
-  {
+  if (w < 1024) {  // k <= 256: one workgroup per block (the wide form's agent-scope release of the digests cost
+                   // more than its 4 -> 2 digest compressions saved: 0.077 -> 0.112 ms per B = 128 step at k = 128)
     ProfScope ps(c, "dah", s);
     const int lr = launch_dah(d_roots, d_dah, (int)(2 * w), (int)nblocks, s);
+    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+  } else {  // k = 512: 2,048 roots, 8 digest compressions per thread in one workgroup -> 2 over eight (0.147 ->
+            // 0.112 ms per two squares)
+    // per-block counters (zeroed once; the kernel leaves them at 0), then n digests of 32 B per block
+    const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255, need = cnt_b + (size_t)nblocks * 2 * w * 32;
+    if (c->done.cap < need) {
+      int rc = ensure(c, c->done, std::max<size_t>(need, 64 * 1024));
+      if (rc) return rc;
+      if (!dev_ok(c, hipMemsetAsync(c->done.p, 0, c->done.cap, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+    }
+    ProfScope ps(c, "dah", s);
+    const int lr = launch_dah_wide(d_roots, d_dah, (unsigned*)c->done.p, (uint8_t*)c->done.p + cnt_b, (int)(2 * w),
+                                   (int)nblocks, s);
     if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
   }
   return CDA_OK;

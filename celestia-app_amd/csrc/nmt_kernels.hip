@@ -309,6 +309,41 @@ __global__ void __launch_bounds__(256) dah_kernel(const uint4* __restrict__ root
   dah_fold_kw(sdig, n, dah + blockIdx.x * 8, sdig + (n + (n + 1) / 2) * 8);
 }
 
+// DAH of a batch, wide form: the root digests by P = ceil(n / 256) workgroups per block, one root per thread, and
+// the fold by the workgroup that finishes a block's digests last (agent-scope acq_rel counter, put back to 0).  The
+// one-workgroup-per-block dah_kernel hashed n / 256 roots per thread first (8 at k = 512) before its fold.
+__global__ void __launch_bounds__(256) dah_wide_kernel(const uint4* __restrict__ roots, uint32_t* __restrict__ dah,
+                                                       unsigned* __restrict__ done, uint32_t* __restrict__ digests,
+                                                       int n, int P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sdig[];  // [n + (n+1)/2][8] digests, then kw rows
+  __shared__ unsigned last;
+  const unsigned b = blockIdx.x / P, part = blockIdx.x % P;
+  if (threadIdx.x == 0) last = 0;
+  const int i = part * 256 + threadIdx.x;
+  if (i < n) {
+    uint32_t L[24], st[8];
+    load_node(roots + ((size_t)b * n + i) * 6, L);
+    dah_leaf_digest(L, st);
+    uint4* dg = reinterpret_cast<uint4*>(digests + ((size_t)b * n + i) * 8);
+    dg[0] = make_uint4(st[0], st[1], st[2], st[3]);
+    dg[1] = make_uint4(st[4], st[5], st[6], st[7]);
+  }
+  __threadfence();  // this thread's digest, released at agent scope before the block's counter moves
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(done + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)P - 1) last = 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the other workgroups' digests
+  const uint4* src = reinterpret_cast<const uint4*>(digests + (size_t)b * n * 8);
+  for (int x = threadIdx.x; x < n * 2; x += blockDim.x) reinterpret_cast<uint4*>(sdig)[x] = src[x];
+  __syncthreads();
+  dah_fold_kw(sdig, n, dah + b * 8, sdig + (n + (n + 1) / 2) * 8);
+  if (threadIdx.x == 0) __hip_atomic_store(done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Small batches (the single block of ProcessProposal, config C2): every tree of the batch in ONE launch.  A
 // 256-thread workgroup takes two trees (waves 0-1 the first, waves 2-3 the second; one workgroup per CU at k = 128).
 // A tree's w leaf records go to LDS
@@ -559,6 +594,22 @@ int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned*
     return -1;
   hipLaunchKernelGGL(trees_lds_kernel, dim3((unsigned)nblocks * w), dim3(256), lds, s,
                      (const uint4*)d_leaves, (uint4*)d_roots, (uint32_t*)d_dah, d_done, (uint32_t*)d_digests, log2w);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_dah_wide(const void* d_roots, void* d_dah, unsigned* d_done, void* d_digests, int n, int nblocks,
+                    hipStream_t s) {
+  if (n < 1 || nblocks < 1) return -2;
+  const size_t lds = ((size_t)n + (n + 1) / 2) * 32 + (size_t)64 * kKwStride * 4;
+  if (lds > 160 * 1024 - 64) return -2;
+  // the dynamic-LDS limit is a per-device attribute: raised on the current device for each launch that needs it
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)dah_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return -1;
+  const int P = (n + 255) / 256;
+  hipLaunchKernelGGL(dah_wide_kernel, dim3((unsigned)nblocks * P), dim3(256), lds, s, (const uint4*)d_roots,
+                     (uint32_t*)d_dah, d_done, (uint32_t*)d_digests, n, P);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
