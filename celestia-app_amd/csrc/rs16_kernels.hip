@@ -8,7 +8,7 @@
 // Design.  One workgroup holds ONE whole codeword in registers: 512 positions x 512-B shards = 256 KiB = 16 waves x
 // 64 lanes x 64 VGPRs.  A lane owns one 64-B unit of 4 positions (unit = 32 GF(2^16) elements bit-sliced into 16
 // plane words, standard polynomial basis of GF(2)[x]/(x^16+x^5+x^3+x^2+1), as the LDS encoder):
-//   lane bits 0..2 = unit u (bytes [64u, 64u + 64) of every shard: 8 lanes read a whole 512-B shard),
+//   lane bits 0..2 = unit u (32 whole elements of every shard: 8 lanes cover a 512-B shard; see pair_in),
 //   lane bits 3, 4, 5 = three position bits (A3, A4, A5), register slot bits R0, R1 = two position bits,
 //   wave bits W0..W3 = four position bits.
 // A layer's butterfly bit is always moved into a register slot, so every butterfly is two register sets of one
@@ -22,16 +22,21 @@
 //   LE  p7:R0 p8:R1 p5:W2 p6:W3                        IFFT d = 7, 8, FFT d = 8, 7
 //       (LC <-> LD <-> LE: register bits <-> wave bits through LDS, 2 rounds of 8 planes, 128 KiB)
 // A layer constant depends on the position bits above d.  When they all sit in registers it is a compile-time
-// value and the multiply is its 16x16 GF(2) matrix as a straight v_bitop3 XOR3 program (~64 VALU); when some sit
-// in wave bits it is wave-uniform (runtime: scalar branches on its 16 bits); when some sit in lane bits (d <= 2) it
-// is per lane (16 lane masks x 16 planes, v_bitop3).  The old LDS encoder paid the per-lane form on 12 of 18 layers
-// and one LDS round trip + barrier per layer; here 6 of 18 layers are per-lane and the state crosses LDS 4 times.
+// value and the multiply is its 16x16 GF(2) matrix as a straight v_bitop3 XOR3 program (~64 VALU); when several
+// sit in lane bits (d <= 1) it is per lane (16 lane masks x 16 planes, v_bitop3).  The old LDS encoder paid the
+// per-lane form on 12 of 18 layers and one LDS round trip + barrier per layer; here 4 of 18 layers are per-lane and
+// the state crosses LDS 4 times.
 //
 // Wave bits W2, W3 are made compile-time by running one kernel body per value (scalar branch at entry), so layers
-// 5..8 (LD, LE) multiply by compile-time constants.  In LC the layer-3/4 constants still depend on W0, W1 (p5, p6).
-// Leopard's skews are GF(2)-affine in the position bits (FFTSkew[j + 2^(i+1)] = FFTSkew[j] ^ temp[i] in
-// FFTInitialize; checked for every layer in tests/test_rs16_affine.py), so such a constant is c_ct ^ w0*t5 ^ w1*t6
-// with c_ct, t5, t6 compile-time: one XOR program plus one more per set runtime bit, no per-bit scalar branches.
+// 5..8 (LD, LE) multiply by compile-time constants.  The other runtime bits above a layer (W0, W1 in LC; lane bit
+// 3 at layer 2 in LB) are split off: Leopard's skews are GF(2)-affine in the position bits (FFTSkew[j + 2^(i+1)] =
+// FFTSkew[j] ^ temp[i] in FFTInitialize; checked for every layer in tests/test_rs16_affine.py), so such a constant
+// is c_ct ^ sum(b_i * t_i) with c_ct, t_i compile-time: one XOR program plus one more per set runtime bit
+// (exec-masked for wave bits, lane-masked for the lane bit), no per-bit scalar branches.
+//
+// Persistent: one workgroup per CU walks codewords blockIdx.x, + gridDim.x, ...; after the last LDS exchange of a
+// codeword each wave streams half of its share of the next codeword into the idle exchange buffer (global_load_lds).
+// DESIGN.md §6 has the measured steps.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
