@@ -27,8 +27,8 @@
 // per-lane form on 12 of 18 layers and one LDS round trip + barrier per layer; here 4 of 18 layers are per-lane and
 // the state crosses LDS 4 times.
 //
-// Wave bits W2, W3 are made compile-time by running one kernel body per value (scalar branch at entry), so layers
-// 5..8 (LD, LE) multiply by compile-time constants.  The other runtime bits above a layer (W0, W1 in LC; lane bit
+// Wave bits W1..W3 are made compile-time by running one kernel body per value (8 bodies, scalar branch at entry), so
+// layers 5..8 (LD, LE) multiply by compile-time constants.  The other runtime bits above a layer (W0 in LC; lane bit
 // 3 at layer 2 in LB) are split off: Leopard's skews are GF(2)-affine in the position bits (FFTSkew[j + 2^(i+1)] =
 // FFTSkew[j] ^ temp[i] in FFTInitialize; checked for every layer in tests/test_rs16_affine.py), so such a constant
 // is c_ct ^ sum(b_i * t_i) with c_ct, t_i compile-time: one XOR program plus one more per set runtime bit
@@ -251,12 +251,12 @@ __device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
     if constexpr (lane_bits_above(Y, D) > 1) {  // per-lane constant (preloaded), generic multiply
       constexpr int slot = lv_slot(INVERSE, D, R);
       muladd_lane(X, Yv, (cx.lv[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu);
-    } else {  // compile-time, plus one term per runtime wave bit (W0, W1) and lane bit 3 above d
-      constexpr int sct = (pos_r(Y, R) + pos_w_ct(Y, OM * 4)) & hi;
+    } else {  // compile-time, plus one term per runtime wave bit (W0) and lane bit 3 above d
+      constexpr int sct = (pos_r(Y, R) + pos_w_ct(Y, OM * 2)) & hi;
       static_assert(cidx<INVERSE, D>(sct) < kCpoly16N, "constant table too short");
       muladd_const<kCpoly16[cidx<INVERSE, D>(sct)]>(X, Yv);
-      constexpr int p8 = pos_of_slot(Y, 8), p9 = pos_of_slot(Y, 9);
-      if constexpr (p8 > D || p9 > D) {
+      constexpr int p8 = pos_of_slot(Y, 8), p9 = -1;
+      if constexpr (p8 > D) {
         uint32_t wv = cx.w;
         asm volatile("" : "+v"(wv));
         if constexpr (p8 > D) muladd_wbit<INVERSE, D, 8, p8>(X, Yv, wv);
@@ -578,16 +578,20 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
   }
 }
 
-// one whole body per value of W2, W3 (scalar branch at entry; each runs to the end, so no control-flow merge with
+// one whole body per value of W1..W3 (scalar branch at entry; each runs to the end, so no control-flow merge with
 // the 64 live state registers follows the specialised layers -- such a merge made the register allocator spill)
 __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  switch (w >> 2) {
+  switch (w >> 1) {
     case 0: body<0>(a, xb, w); break;
     case 1: body<1>(a, xb, w); break;
     case 2: body<2>(a, xb, w); break;
-    default: body<3>(a, xb, w); break;
+    case 3: body<3>(a, xb, w); break;
+    case 4: body<4>(a, xb, w); break;
+    case 5: body<5>(a, xb, w); break;
+    case 6: body<6>(a, xb, w); break;
+    default: body<7>(a, xb, w); break;
   }
 }
 
