@@ -681,6 +681,110 @@ def sum_over_ranks(x, world, backend, dev):
     return float(t.item())
 
 
+# ---- config C5's product path at N > 1: one k=512 square over all devices of the node, RCCL exchange ----------------
+# The driver's multi-GPU command is `bench.py --gpus N` (one rank per GPU).  After the timed block-batch loop, rank 0
+# hands one k=512 square to cda_multi_extend_commit_split_device over the devices the ranks use (ncclCommInitAll +
+# one grouped send/recv exchange + a gather: csrc/split.cpp) and reports it beside G = 1.  It runs in a helper
+# process that rank 0 starts BEFORE anything touches the GPU (no fork/exec from a GPU process), waiting on a pipe;
+# the other ranks sit in a CPU (gloo) barrier meanwhile, so no RCCL kernel of theirs spins on the devices.  A
+# failure or a hang of the helper becomes an "error" field, never the headline's exit code.
+K512_SPLIT_TIMEOUT_S = 240
+
+
+class SplitHelper:
+    def __init__(self, ndev, dry_run):
+        import subprocess
+        env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+        cmd = [sys.executable, os.path.abspath(__file__), "--k512-split-helper", str(ndev)]
+        if dry_run:
+            cmd.append("--dry-run")
+        self.p = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+
+    def run(self, timeout=K512_SPLIT_TIMEOUT_S):
+        import subprocess
+        t0 = time.perf_counter()
+        try:
+            out, _ = self.p.communicate("go\n", timeout=timeout)
+        except subprocess.TimeoutExpired:
+            self.p.kill()
+            self.p.communicate()
+            return {"error": f"k=512 split helper timed out after {timeout} s (killed)"}
+        lines = [l for l in out.splitlines() if l.startswith("{")]
+        if self.p.returncode != 0 or not lines:
+            return {"error": f"k=512 split helper exited {self.p.returncode}", "tail": out[-400:]}
+        r = json.loads(lines[-1])
+        r["helper_wall_s"] = round(time.perf_counter() - t0, 2)
+        return r
+
+    def close(self):
+        if self.p.poll() is None:
+            try:
+                self.p.communicate("quit\n", timeout=30)
+            except Exception:
+                self.p.kill()
+
+
+def split_measure(devices, k=512, reps=10, warmup=2, dev_mask_note=""):
+    """One k-square over `devices` through cda_multi_extend_commit_split_device (G = len(devices)), and over the
+    first device alone (G = 1), each with device-resident ODS slabs; per-call times (the call returns the 4k roots
+    and the DAH on the host), the DAH checked against tests/golden/bench_digests.json."""
+    import torch
+    import cda
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")))[f"k{k}"][str(0xC0FFEE)]
+    rows = gen_ods(k, 0xC0FFEE).reshape(k, k, 512)
+    out = {"k": k, "devices": list(devices), "G": len(devices), "dah_golden": want}
+    for label, devs in (("G1", devices[:1]), (f"G{len(devices)}", devices)):
+        if label == "G1" and len(devices) == 1 and "G1" in out:
+            continue
+        G = len(devs)
+        rp = k // G
+        mask = 0
+        for d in devs:
+            mask |= 1 << d
+        t0 = time.perf_counter()
+        m = cda.MultiContext(mask)
+        slabs = [torch.from_numpy(np.ascontiguousarray(rows[g * rp:(g + 1) * rp])).to(f"cuda:{d}")
+                 for g, d in enumerate(devs)]
+        for d in devs:
+            torch.cuda.synchronize(d)
+        ptrs = [s.data_ptr() for s in slabs]
+        _, _, dah = m.extend_commit_split_device(k, ptrs)  # first call: ncclCommInitAll when G > 1
+        first_s = time.perf_counter() - t0
+        for _ in range(warmup):
+            m.extend_commit_split_device(k, ptrs)
+        ts = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            _, _, dah = m.extend_commit_split_device(k, ptrs)
+            ts.append((time.perf_counter() - t1) * 1e3)
+        out[label] = {"ms_per_square": round(min(ts), 3), "ms_median": round(float(np.median(ts)), 3),
+                      "dah_matches_golden": dah.hex() == want, "init_and_first_call_s": round(first_s, 3)}
+        m.close()
+        del slabs
+    gN = out.get(f"G{len(devices)}")
+    if gN and len(devices) > 1:
+        out["speedup_vs_G1"] = round(out["G1"]["ms_median"] / gN["ms_median"], 2)
+    out["note"] = ("cda_multi_extend_commit_split_device: rows over devices, one RCCL grouped send/recv exchange of the "
+                   "top half (shares + leaf records), column pass, gather + DAH on device 0; per-call host time, roots "
+                   "and DAH returned to the host" + dev_mask_note)
+    return out
+
+
+def split_helper_main(args):
+    """--k512-split-helper N: wait for "go" on stdin, then time config C5's split over devices 0..N-1."""
+    line = sys.stdin.readline().strip()
+    if line != "go":
+        return
+    if args.dry_run:
+        print(json.dumps({"dry_run": True, "G": args.k512_split_helper}), flush=True)
+        return
+    try:
+        res = split_measure(list(range(args.k512_split_helper)))
+    except Exception as e:  # reported in the bench line, never raised into the bench's exit code
+        res = {"error": f"{type(e).__name__}: {e}"}
+    print(json.dumps(res), flush=True)
+
+
 VALU_CYCLES_PER_WAVE_INSTR = 2  # wave64 on a SIMD-32 (MI355X_MICROARCH.md, execution model)
 
 
@@ -700,7 +804,11 @@ def main():
     ap.add_argument("--workload", choices=["block_batch", "split"], default="block_batch",
                     help="block_batch: B independent blocks per GPU (default, BASELINE metric); "
                          "split: ONE k-square split over all ranks with an RCCL all-to-all (config C5, --k 512)")
+    ap.add_argument("--k512-split-helper", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--no-k512-split", action="store_true", help="skip config C5's split after the timed loop")
     args = ap.parse_args()
+    if args.k512_split_helper:
+        return split_helper_main(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     if args.workload == "split":
@@ -709,17 +817,49 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # config C5 at N > 1: the helper process starts before this process touches the GPU (SplitHelper)
+    helper = None
+    if rank == 0 and world > 1 and not args.no_k512_split:
+        helper = SplitHelper(split_devices(world), args.dry_run)
+    try:
+        return bench_main(args, world, rank, local, helper)
+    finally:
+        if helper is not None:
+            helper.close()
+
+
+def split_devices(world):
+    """Distinct devices the ranks use (rank r -> device r % device_count; device_count does not initialise HIP)."""
+    try:
+        import torch
+        ndev = torch.cuda.device_count()
+    except Exception:
+        ndev = 0
+    n = min(world, ndev) if ndev else world
+    while n & (n - 1):  # the split takes a power of two of devices
+        n &= n - 1
+    return max(1, n)
+
+
+def bench_main(args, world, rank, local, helper):
     dev, backend, shared = dist_setup(world, local, args.dry_run)
     import torch
     import torch.distributed as dist
+    cpu_group = dist.new_group(backend="gloo") if world > 1 else None
     if args.dry_run:
         if world > 1:
             dist.barrier()
         ranks = sum_over_ranks(1.0, world, backend, dev)
         t = max_over_ranks(float(rank), world, backend, dev)
+        split = None
+        if world > 1:
+            dist.barrier(group=cpu_group)
+            if helper is not None:
+                split = helper.run()
+            dist.barrier(group=cpu_group)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(ranks), "max_rank": int(t),
-                              "backend": backend}), flush=True)
+                              "backend": backend, **({"k512_split": split} if split else {})}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -814,6 +954,19 @@ def main():
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
     }
     gpu = {}
+    # config C5's product path: one k=512 square over every device the ranks use (G = N; helper process, RCCL) and
+    # on one device (G = 1); at N = 1 in this process
+    if world > 1:
+        torch.cuda.synchronize(dev)
+        dist.barrier(group=cpu_group)
+        if helper is not None:
+            result["k512_split"] = helper.run()
+        dist.barrier(group=cpu_group)
+    elif not args.no_k512_split:
+        try:
+            result["k512_split"] = split_measure([dev.index])
+        except Exception as e:  # reported, never the headline's exit code
+            result["k512_split"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_extras:
         del d_eds, d_roots, d_ods
         torch.cuda.empty_cache()
@@ -842,8 +995,10 @@ def check_dahs(dah, k, B, rank, nd):
     seeds); replicas of one square must agree too."""
     path = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
     want = json.load(open(path)).get(f"k{k}", {}) if os.path.exists(path) else {}
-    if os.environ.get("CDA_BENCH_DIAG_BUILD"):  # a diagnostic library build (e.g. RS without arithmetic): timing only
-        return {"blocks_checked_vs_golden": 0, "skipped": "CDA_BENCH_DIAG_BUILD set: diagnostic library, not a result"}
+    import cda
+    info = cda.build_info()
+    if not info.startswith("release"):  # the loaded library says it is a diagnostic build: timing only, no result
+        return {"blocks_checked_vs_golden": 0, "skipped": f"diagnostic library ({info}), not a result"}
     checked = 0
     for b in range(B):
         got = bytes(dah[b]).hex()

@@ -100,6 +100,7 @@ def lib():
                 "cda_free": (None, [P]),
                 "cda_strerror": (ctypes.c_char_p, [I32]),
                 "cda_last_device_error": (ctypes.c_char_p, [P]),
+                "cda_build_info": (ctypes.c_char_p, []),
                 "cda_rs_encode": (I32, [P, U32, U32, P, P]),
                 "cda_rs_decode": (I32, [P, U32, U32, P, P]),
                 "cda_rs_max_chunks": (I64, []),
@@ -145,6 +146,11 @@ def lib():
                 f.argtypes = args
             _lib = L
     return _lib
+
+
+def build_info():
+    """cda_build_info(): "release gfx950", or "diagnostic gfx950 <tags>" for a diagnostic library build."""
+    return lib().cda_build_info().decode()
 
 
 def strerror(code):

@@ -54,6 +54,9 @@ int launch_rs_encode8(const RsJob& job, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
 // register-resident GF(2^16) encoder for k = 512 (rs16_kernels.hip)
 bool rs16_reg_eligible(const RsJob& j);
+// diagnostic-build tags ("" in a release build; cda_build_info)
+const char* rs16_diag_tag();
+const char* rs8_diag_tag();
 int rs16_reg_init(int device);
 int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t s);
 int launch_leaf_hash(const uint8_t* d_eds, void* d_leaf_nodes, unsigned long long* d_status, int k, int nblocks,

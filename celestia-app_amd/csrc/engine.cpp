@@ -389,6 +389,16 @@ const char* cda_strerror(int code) {
 
 const char* cda_last_device_error(cda_ctx* c) { return c ? c->last_err.c_str() : ""; }
 
+const char* cda_build_info(void) {
+  static const std::string info = [] {
+    std::string d;
+    for (const char* t : {rs8_diag_tag(), rs16_diag_tag()})
+      if (*t) d += (d.empty() ? "" : ",") + std::string(t);
+    return d.empty() ? std::string("release gfx950") : "diagnostic gfx950 " + d;
+  }();
+  return info.c_str();
+}
+
 int64_t cda_rs_max_chunks(void) { return (int64_t)32768 * 32768; }
 const char* cda_rs_name(void) { return "Leopard"; }
 int cda_rs_validate_chunk_size(int64_t chunk_size) {

@@ -392,8 +392,15 @@ struct Args {
   long long cpy_blk, cpy_cw, cpy_sh;
   const uint16_t* cpoly;
   int cw_per_blk, slices, total;  // total = codewords of the launch
-  int mode;  // diagnostics (CDA_RS16_MODE): 0 = encode; 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores
 };
+
+// Diagnostic builds only (scripts/gpu_rs16_diag.sh compiles a separate library with -DCDA_RS16_DIAG_MODE=N):
+// 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores.  A release build is always 0 (encode) -- no
+// environment switch can change what the product path computes; cda_build_info() names a diag build.
+#ifndef CDA_RS16_DIAG_MODE
+#define CDA_RS16_DIAG_MODE 0
+#endif
+constexpr int kMode = CDA_RS16_DIAG_MODE;
 
 // Coalesced shard access.  Leopard's GF(2^16) shard layout pairs element e of each 64-B block with bytes e (low)
 // and 32 + e (high).  Lane u (= lane & 7) of a position moves the 16-B chunks at u*16 + 128q, q = 0..3, so the 8
@@ -479,7 +486,7 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
       if (r < 2 && pre) {
         q0 = xw[(r * 4 + 0) * 64 + lane], q1 = xw[(r * 4 + 1) * 64 + lane];
         q2 = xw[(r * 4 + 2) * 64 + lane], q3 = xw[(r * 4 + 3) * 64 + lane];
-      } else if (a.mode < 2) {  // modes >= 2: synthetic data, no loads
+      } else if (kMode < 2) {  // modes >= 2: synthetic data, no loads
         q0 = p[0], q1 = p[8], q2 = p[16], q3 = p[24];
       } else {
         q0 = make_uint4(s, lane, w, r), q1 = make_uint4(lane * 3, s ^ 5, 7, w), q2 = q0, q3 = q1;
@@ -504,7 +511,7 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
     }
     const int gn = g + (int)gridDim.x;
     pre = false;
-    if (a.mode != 1) {
+    if (kMode != 1) {
       // IFFT, D = 1 .. m/2
       layer<LA, true, 0, OM>(E, cx);
       layer<LA, true, 1, OM>(E, cx);
@@ -539,7 +546,7 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
           for (int q = 0; q < 4; q++)
             __builtin_amdgcn_global_load_lds((glb_ptr)(sp + 128 * q), (lds_ptr)(xw + (r * 4 + q) * 64), 16, 0, 0);
         }
-        pre = a.mode == 0;
+        pre = kMode == 0;
       }
       layer<LC, false, 4, OM>(E, cx);
       layer<LC, false, 3, OM>(E, cx);
@@ -549,7 +556,7 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
       layer<LA, false, 1, OM>(E, cx);
       layer<LA, false, 0, OM>(E, cx);
     }
-    if (a.mode == 3) continue;
+    if (kMode == 3) continue;
     // parity shard s = point s
     const SliceMasks ko = slice_masks();
 #pragma unroll
@@ -597,6 +604,16 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
 
 }  // namespace r16
 
+const char* rs16_diag_tag() {
+#if CDA_RS16_DIAG_MODE != 0
+#define CDA_STR2(x) #x
+#define CDA_STR(x) CDA_STR2(x)
+  return "rs16_mode=" CDA_STR(CDA_RS16_DIAG_MODE);
+#else
+  return "";
+#endif
+}
+
 bool rs16_reg_eligible(const RsJob& j) { return j.k == r16::M && j.shard_len % 512 == 0; }
 
 int rs16_reg_init(int device) {
@@ -638,11 +655,6 @@ int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t 
   a.cpoly = d_cpoly;
   a.cw_per_blk = j.cw_per_blk;
   a.slices = j.shard_len / 512;
-  static const int mode = [] {
-    const char* e = getenv("CDA_RS16_MODE");
-    return e ? atoi(e) : 0;
-  }();
-  a.mode = mode;
   const long long total = (long long)j.nblk * j.cw_per_blk * a.slices;
   if (total <= 0 || total > 0x7FFFFFFF) return -2;
   a.total = (int)total;

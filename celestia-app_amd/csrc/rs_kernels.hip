@@ -852,6 +852,14 @@ int rs16_init_device_tables(int device) {
   return 0;
 }
 
+const char* rs8_diag_tag() {
+#ifdef CDA_RS8_DIAG_NOCOMPUTE
+  return "rs8_nocompute";
+#else
+  return "";
+#endif
+}
+
 int launch_rs_encode16(const RsJob& j, hipStream_t s) {
   if (j.k < 1 || j.k > 32768 || j.shard_len % 64 != 0) return -2;
   int dev = 0;

@@ -73,6 +73,9 @@ void cda_free(cda_ctx* ctx);
 const char* cda_strerror(int code);
 /* Last HIP error string recorded by the context (for CDA_E_DEVICE). */
 const char* cda_last_device_error(cda_ctx* ctx);
+/* "release gfx950", or "diagnostic gfx950 <tags>" for a library built with a diagnostic define that changes what
+ * the kernels compute (timing experiments only; no environment variable can do that to a release build). */
+const char* cda_build_info(void);
 
 /* ---- rsmt2d.Codec (LeoRSCodec replacement) ---------------------------- */
 /* Replaces rsmt2d.LeoRSCodec selected by appconsts.DefaultCodec

@@ -1,0 +1,88 @@
+"""The consensus-path call as go/cda.ExtendSharesOn makes it (go/cda/extend.go:42-48): one k=128 block per
+cda_extend_commit call, the shares freshly copied into a new flat buffer (outside the timed call, as Go's flatten
+runs before the cgo call) and a NEW, untouched 32 MiB EDS buffer per call (np.empty: fresh mmap'd pages, as a large
+Go make()).  Reports min / median per form, plus host first-touch copy rates into fresh pages by thread count and
+the box's transparent-huge-page setting -- what bounds a fresh-buffer D2H."""
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "celestia-app_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+import bench  # noqa: E402
+import cda  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+ctx = cda.Context(0)
+k, w = 128, 256
+ods = bench.gen_ods(k, 0xC0FFEE).reshape(k * k, 512)
+eds_ref, rr_ref, cr_ref, dah_ref = ctx.extend_commit(ods)
+
+
+def series(want_eds, fresh_out):
+    out = []
+    keep = np.ones((w * w, 512), np.uint8)
+    for i in range(reps + 2):
+        src = ods.copy()
+        t0 = time.perf_counter()
+        if fresh_out:
+            eds, rr, cr, dah = ctx.extend_commit(src, want_eds=want_eds)
+        else:
+            eds, rr, cr, dah = ctx.extend_commit_batch(src[None], want_eds=want_eds, eds_out=keep[None] if want_eds
+                                                       else None)
+            dah = bytes(dah[0])
+        el = (time.perf_counter() - t0) * 1e3
+        if dah != dah_ref:
+            raise RuntimeError("DAH mismatch")
+        if want_eds and i == reps + 1:
+            got = eds if fresh_out else keep
+            if not np.array_equal(got.reshape(eds_ref.shape), eds_ref):
+                raise RuntimeError("EDS mismatch")
+        if i >= 2:
+            out.append(el)
+    return {"min": round(min(out), 3), "median": round(float(np.median(out)), 3), "max": round(max(out), 3)}
+
+
+res = {"reps": reps}
+res["fresh_with_eds"] = series(True, True)
+res["fresh_roots_only"] = series(False, True)
+res["reused_with_eds"] = series(True, False)
+res["reused_roots_only"] = series(False, False)
+print(json.dumps(res), flush=True)
+
+# host side: first-touch copies into fresh pages
+N = 32 << 20
+src = torch.empty(N, dtype=torch.uint8).pin_memory().numpy()
+src[:] = 7
+host = {}
+for T in (1, 2, 4, 8, 12, 16):
+    times = []
+    for _ in range(5):
+        dst = np.empty(N, np.uint8)
+        bounds = [(N * i // T, N * (i + 1) // T) for i in range(T)]
+        t0 = time.perf_counter()
+        ths = [threading.Thread(target=lambda lo, hi: np.copyto(dst[lo:hi], src[lo:hi]), args=b) for b in bounds]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        times.append(time.perf_counter() - t0)
+        del dst
+    host[str(T)] = {"fresh_gbs_best": round(N / min(times) / 1e9, 1), "fresh_gbs_median": round(N / float(np.median(times)) / 1e9, 1)}
+warm = np.empty(N, np.uint8)
+warm.fill(1)
+t0 = time.perf_counter()
+np.copyto(warm, src)
+host["1_warm_gbs"] = round(N / (time.perf_counter() - t0) / 1e9, 1)
+thp = {}
+for f in ("enabled", "defrag"):
+    try:
+        thp[f] = open(f"/sys/kernel/mm/transparent_hugepage/{f}").read().strip()
+    except OSError:
+        thp[f] = None
+print(json.dumps({"host_first_touch_copy": host, "thp": thp, "affinity": len(os.sched_getaffinity(0))}), flush=True)

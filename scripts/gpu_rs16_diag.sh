@@ -1,12 +1,14 @@
 #!/bin/bash
 # GF(2^16) register encoder diagnostics at k=512: timing by mode (encode / memory only / no loads / no memory), the
-# LDS encoder for comparison, and rocprofv3 PMC passes of the encode mode.
+# LDS encoder for comparison, and rocprofv3 PMC passes of the encode mode.  The mode libraries are built beforehand
+# on the CPU side: for m in 0 1 2 3; do make -C celestia-app_amd BUILD=build_m$m OUT=../ab/libcda_rs16m$m.so \
+#   EXTRA=-DCDA_RS16_DIAG_MODE=$m; done
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/rs16
 mkdir -p "$OUT"
 for m in 0 1 2 3; do
-  echo "mode $m"; CDA_RS16_MODE=$m timeout -k 10 120 python3 -u scripts/rs16_probe.py 20 || exit $?
+  echo "mode $m"; CDA_LIB=ab/libcda_rs16m$m.so timeout -k 10 120 python3 -u scripts/rs16_probe.py 20 || exit $?
 done
 echo "lds"; CDA_RS16=lds timeout -k 10 120 python3 -u scripts/rs16_probe.py 20 || exit $?
 cd /tmp && export TMPDIR=/tmp

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/rs16d
 mkdir -p "$OUT"
 for m in 0 1 2 3; do
-  echo "mode $m $(CDA_RS16_MODE=$m timeout -k 10 120 python3 -u scripts/rs16_probe.py 20)" || exit 1
+  echo "mode $m $(CDA_LIB=ab/libcda_rs16m$m.so timeout -k 10 120 python3 -u scripts/rs16_probe.py 20)" || exit 1
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU --kernel-trace --output-format csv -d "$OUT/sq" -o run -- python3 $R/scripts/rs16_probe.py 5 > "$OUT/sq.log" 2>&1 || exit 1

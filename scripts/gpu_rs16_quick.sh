@@ -8,4 +8,4 @@ run() {
 }
 mkdir -p gpurun_out
 run ff16_parity 300 python -u -m pytest tests/test_gpu_parity.py tests/test_split_capi_gpu.py -x -q --timeout 120 --timeout-method thread -k "ff16 or 512 or split"
-for m in 0 3 4 5 6; do echo "mode $m"; CDA_RS16_MODE=$m timeout -k 10 120 python3 -u scripts/rs16_probe.py 20 || exit $?; done
+for m in 0 3 4 5 6; do echo "mode $m"; CDA_LIB=ab/libcda_rs16m$m.so timeout -k 10 120 python3 -u scripts/rs16_probe.py 20 || exit $?; done

@@ -24,11 +24,26 @@ def _run_bench(*args):
 def test_bench_spawns_two_ranks():
     r = _run_bench("--gpus", "2", "--dry-run")
     assert r["n_gpus"] == 2 and r["ranks_seen"] == 2 and r["max_rank"] == 1
+    # config C5's split helper (started before the GPU is touched, run between two CPU barriers) answered
+    assert r["k512_split"] == {"dry_run": True, "G": 2, "helper_wall_s": r["k512_split"]["helper_wall_s"]}
 
 
 def test_bench_spawns_four_ranks():
     r = _run_bench("--gpus", "4", "--dry-run")
     assert r["n_gpus"] == 4 and r["ranks_seen"] == 4
+    assert r["k512_split"]["G"] == 4
+
+
+def test_bench_split_helper_failure_is_a_field():
+    """A helper that cannot run becomes an error field, not the bench's exit code."""
+    sys.path.insert(0, ROOT)
+    import bench
+    h = bench.SplitHelper(2, dry_run=False)
+    h.p.stdin.write("quit\n")  # the helper leaves without answering
+    h.p.stdin.flush()
+    h.p.wait(timeout=60)
+    r = h.run(timeout=5)
+    assert "error" in r
 
 
 def test_cpu_throughput_sampler():
