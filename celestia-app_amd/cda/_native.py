@@ -42,7 +42,7 @@ AXIS_COL = 1
 
 # Every symbol declared in include/cda.h (checked by tests/test_abi.py).
 EXPORTS = [
-    "cda_init", "cda_free", "cda_strerror", "cda_last_device_error",
+    "cda_init", "cda_free", "cda_strerror", "cda_last_device_error", "cda_build_info",
     "cda_rs_encode", "cda_rs_decode", "cda_rs_max_chunks", "cda_rs_name", "cda_rs_validate_chunk_size",
     "cda_extend_commit", "cda_extend_commit_batch", "cda_extend_commit_device", "cda_commit_eds",
     "cda_dah_hash", "cda_nmt_axis_root", "cda_repair", "cda_repair_device",
