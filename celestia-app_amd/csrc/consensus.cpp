@@ -1,0 +1,421 @@
+// consensus.cpp — ONE block through host buffers, shaped for the consensus path.
+//
+// PrepareProposal and ProcessProposal extend one block per call (app/prepare_proposal.go:65-93,
+// app/process_proposal.go:137-151 -> da.ExtendShares + da.NewDataAvailabilityHeader,
+// pkg/da/data_availability_header.go:44-75), and go/cda.ExtendSharesOn hands libcda a freshly copied share buffer
+// and a NEW 4k^2 x 512 B EDS slice per call (go/cda/extend.go:42-48).  A plain pageable hipMemcpy into such a slice
+// pins it page by page in the calling thread (first-touch faults included), so the old serial form -- H2D, whole
+// pipeline, one D2H -- spent most of its time in the host side of the copies.  Here every host byte moves through
+// pinned buffers of this context with a pool of copy threads, and the copies overlap the device work:
+//
+//   ODS    : the caller's rows are copied into a pinned slab by the pool, one row band at a time; each band's DMA is
+//            issued as soon as it is staged, and the RS row pass of that band runs as soon as its DMA lands.
+//   Q0     : the EDS's top-left quadrant IS the ODS (rsmt2d copies the shares in): the pool copies it host to host
+//            from the caller's ODS into the caller's EDS -- it never crosses PCIe.
+//   Q1     : each band's right halves come back (one 2-D DMA per band) right after that band's row pass.
+//   Q2|Q3  : the bottom half comes back in chunks right after the column pass, while the leaf hashing, the trees and
+//            the DAH run on the compute stream; the pool copies each chunk into the caller's slice as it lands.
+//   pages  : while the device works, the pool touches the caller's (possibly never-touched) output pages, so the
+//            first-touch faults are off the critical path and spread over the pool's threads.
+// Pinned caller buffers (cda_host_alloc / hipHostRegister) skip the staging: DMA straight to / from them.
+// k <= 256 (pinned slabs of up to 32 + 96 MiB per context); larger squares and profiling runs use the serial form.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ctx.h"
+
+namespace cda {
+
+// Copy workers of one context.  A job is an ordered list of tasks; workers (and, once it has issued the device
+// work, the calling thread) take them in order.  Tasks that need a DMA to land wait for it themselves.  Each job is
+// its own object: a worker that wakes late only ever draws from the job it picked up, whose counter is spent.
+class CopyPool {
+ public:
+  CopyPool(const cda_ctx* c, int n) {
+    th_.reserve(n);
+    try {
+      for (int i = 0; i < n; i++)
+        th_.emplace_back([this, c] {
+          bind_helper_thread(c);
+          loop();
+        });
+    } catch (...) {
+      shutdown();
+      throw;
+    }
+  }
+  ~CopyPool() { shutdown(); }
+  void start(std::vector<std::function<void()>>* tasks) {
+    auto j = std::make_shared<Job>();
+    j->tasks = tasks;
+    j->n = tasks->size();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      cur_ = j;
+      ++gen_;
+    }
+    cv_.notify_all();
+  }
+  // the calling thread takes tasks too, then waits until every task of the job has finished
+  void help_and_wait() {
+    std::shared_ptr<Job> j;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      j = cur_;
+      cur_.reset();
+    }
+    if (!j) return;
+    run(*j);
+    while (j->done.load(std::memory_order_acquire) < j->n) std::this_thread::yield();
+  }
+
+ private:
+  struct Job {
+    std::vector<std::function<void()>>* tasks = nullptr;
+    size_t n = 0;
+    std::atomic<size_t> next{0}, done{0};
+  };
+  static void run(Job& j) {
+    for (;;) {
+      const size_t i = j.next.fetch_add(1);
+      if (i >= j.n) return;
+      (*j.tasks)[i]();
+      j.done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void loop() {
+    unsigned seen = 0;
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        j = cur_;
+      }
+      if (j) run(*j);
+    }
+  }
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::shared_ptr<Job> cur_;
+  unsigned gen_ = 0;
+  bool stop_ = false;
+};
+
+struct Consensus {
+  static constexpr int kMaxBands = 8, kMaxChunks = 16;
+  CopyPool* pool = nullptr;
+  uint8_t* pin_in = nullptr;   // ODS staging (k^2 x 512)
+  uint8_t* pin_out = nullptr;  // Q1 (k x k shares) | bottom half (k x 2k shares)
+  uint8_t* pin_res = nullptr;  // 4k root records | DAH | status
+  size_t cap_in = 0, cap_out = 0, cap_res = 0;
+  hipEvent_t ev_in[kMaxBands] = {}, ev_rows[kMaxBands] = {}, ev_q1[kMaxBands] = {}, ev_cols = nullptr,
+             ev_bot[kMaxChunks] = {}, ev_done = nullptr;
+  ~Consensus() {
+    delete pool;
+    for (uint8_t* p : {pin_in, pin_out, pin_res})
+      if (p) (void)hipHostFree(p);
+    for (int i = 0; i < kMaxBands; i++)
+      for (hipEvent_t e : {ev_in[i], ev_rows[i], ev_q1[i]})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_bot)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_cols, ev_done})
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+void free_consensus(cda_ctx* c) {
+  delete c->cons;
+  c->cons = nullptr;
+}
+
+bool consensus_eligible(const cda_ctx* c, uint32_t k) { return c->consensus && !c->prof && k <= 256; }
+
+namespace {
+
+bool pinned_host(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not an error here
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+int grow_pinned(cda_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
+  if (cap >= need) return CDA_OK;
+  fault_point("alloc");
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  if (!dev_ok(c, hipHostMalloc((void**)&p, need, hipHostMallocDefault), "hipHostMalloc")) return CDA_E_DEVICE;
+  cap = need;
+  return CDA_OK;
+}
+
+int get_consensus(cda_ctx* c, Consensus*& out) {
+  if (!c->cons) {
+    auto* s = new Consensus();
+    bool ok = true;
+    for (int i = 0; i < Consensus::kMaxBands && ok; i++)
+      ok = hipEventCreateWithFlags(&s->ev_in[i], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s->ev_rows[i], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s->ev_q1[i], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < Consensus::kMaxChunks && ok; i++)
+      ok = hipEventCreateWithFlags(&s->ev_bot[i], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&s->ev_cols, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      delete s;
+      c->last_err = "consensus path: event creation failed";
+      return CDA_E_DEVICE;
+    }
+    c->cons = s;
+  }
+  if (!c->cons->pool) {
+    fault_point("thread");
+    int n = 7;  // + the calling thread; measured: scripts/consensus_probe.py
+    if (const char* e = getenv("CDA_COPY_THREADS")) n = std::max(1, std::min(64, atoi(e)));
+    c->cons->pool = new CopyPool(c, n);
+  }
+  out = c->cons;
+  return CDA_OK;
+}
+
+// spin until a host-side counter reaches `need` (a DMA's event has been recorded), or the call aborts
+bool wait_count(const std::atomic<int>& cnt, int need, const std::atomic<bool>& abort) {
+  while (cnt.load(std::memory_order_acquire) < need) {
+    if (abort.load(std::memory_order_relaxed)) return false;
+    std::this_thread::yield();
+  }
+  return true;
+}
+
+bool wait_event(hipEvent_t e, std::atomic<bool>& abort) {
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return true;
+    if (r != hipErrorNotReady) {
+      abort.store(true);
+      return false;
+    }
+    if (abort.load(std::memory_order_relaxed)) return false;
+    std::this_thread::yield();
+  }
+}
+
+void touch_pages(uint8_t* p, size_t n) {  // first-touch a range of the caller's output (zero bytes: overwritten later)
+  volatile uint8_t* v = p;
+  for (size_t o = 0; o < n; o += 4096) v[o] = 0;
+  if (n) v[n - 1] = 0;
+}
+
+}  // namespace
+
+// The caller holds the context lock.  One block of width k (k <= 256): ods host (k^2 x 512), eds_or_null host
+// (4k^2 x 512), roots / dah / err as cda_extend_commit_batch.
+int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
+                    uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  const uint32_t w = 2 * k;
+  const size_t S = CDA_SHARE, rowS = (size_t)k * S, erowS = (size_t)w * S;
+  const size_t ods_b = (size_t)k * rowS, eds_b = (size_t)w * erowS, q1_b = ods_b, bot_b = (size_t)k * erowS;
+  const size_t roots_b = (size_t)2 * w * CDA_REC_BYTES, res_b = roots_b + 32 + 8;
+  const size_t cells = (size_t)w * w;
+  Consensus* X = nullptr;
+  int rc;
+  if ((rc = ensure_pipeline(c)) || (rc = get_consensus(c, X)) || (rc = ensure(c, c->ods, ods_b)) ||
+      (rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->roots, roots_b)) || (rc = ensure(c, c->dah, 32)) ||
+      (rc = ensure(c, c->status, 8)) || (rc = ensure(c, c->leaf, cells * CDA_REC_BYTES)) ||
+      (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)))
+    return rc;
+  const bool in_pinned = pinned_host(ods);
+  const bool want = eds_or_null != nullptr;
+  const bool out_pinned = want && pinned_host(eds_or_null);
+  if ((!in_pinned && (rc = grow_pinned(c, X->pin_in, X->cap_in, ods_b))) ||
+      (want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + bot_b))) ||
+      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)))
+    return rc;
+
+  // bands of the row pass (an even number of rows each: the FF8 encoder takes codeword pairs) and chunks of the
+  // bottom half's copy-out
+  const uint32_t nband = k >= 16 ? 4 : 1, kb = k / nband;
+  const uint32_t nchunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, bot_b >> 20));
+  const uint8_t* src_in = in_pinned ? ods : X->pin_in;
+  uint8_t* d_ods = (uint8_t*)c->ods.p;
+  uint8_t* d_eds = (uint8_t*)c->eds.p;
+  uint8_t* pin_q1 = X->pin_out;
+  uint8_t* pin_bot = X->pin_out ? X->pin_out + q1_b : nullptr;
+
+  std::atomic<bool> abort{false};
+  std::atomic<int> staged[Consensus::kMaxBands];
+  std::atomic<int> q1_rec{0}, bot_rec{0};
+  const size_t band_b = (size_t)kb * rowS;
+  const int pieces_per_band = band_b >= ((size_t)1 << 20) ? 4 : 1;
+  for (uint32_t b = 0; b < nband; b++) staged[b].store(in_pinned ? 0 : pieces_per_band);
+
+  std::vector<std::function<void()>> tasks;
+  tasks.reserve(128);
+  if (!in_pinned)  // ODS rows -> pinned slab, band by band
+    for (uint32_t b = 0; b < nband; b++)
+      for (int q = 0; q < pieces_per_band; q++) {
+        const size_t lo = b * band_b + band_b * q / pieces_per_band, hi = b * band_b + band_b * (q + 1) / pieces_per_band;
+        tasks.emplace_back([=, &staged] {
+          memcpy(X->pin_in + lo, ods + lo, hi - lo);
+          staged[b].fetch_sub(1, std::memory_order_acq_rel);
+        });
+      }
+  if (want) {
+    if (!out_pinned)  // first touch of the bottom half while the device works
+      for (uint32_t j = 0; j < 2 * nchunk; j++) {
+        const size_t lo = bot_b * j / (2 * nchunk), hi = bot_b * (j + 1) / (2 * nchunk);
+        tasks.emplace_back([=] { touch_pages(eds_or_null + k * erowS + lo, hi - lo); });
+      }
+    // Q0 = the shares, host to host (and the first touch of each row's Q1 half)
+    const uint32_t rows_per_task = std::max<uint32_t>(1, (uint32_t)(((size_t)512 << 10) / rowS));
+    for (uint32_t r0 = 0; r0 < k; r0 += rows_per_task)
+      tasks.emplace_back([=] {
+        for (uint32_t r = r0; r < std::min(k, r0 + rows_per_task); r++) {
+          if (!out_pinned) touch_pages(eds_or_null + r * erowS + rowS, rowS);
+          memcpy(eds_or_null + r * erowS, ods + r * rowS, rowS);
+        }
+      });
+    if (!out_pinned) {
+      for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its 2-D DMA has landed
+        for (uint32_t r0 = b * kb; r0 < (b + 1) * kb; r0 += rows_per_task)
+          tasks.emplace_back([=, &q1_rec, &abort] {
+            if (!wait_count(q1_rec, (int)b + 1, abort) || !wait_event(X->ev_q1[b], abort)) return;
+            for (uint32_t r = r0; r < std::min((b + 1) * kb, r0 + rows_per_task); r++)
+              memcpy(eds_or_null + r * erowS + rowS, pin_q1 + r * rowS, rowS);
+          });
+      for (uint32_t j = 0; j < nchunk; j++) {  // bottom-half chunk j, two tasks each
+        const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk, mid = (lo + hi) / 2;
+        for (int h = 0; h < 2; h++) {
+          const size_t a = h ? mid : lo, z = h ? hi : mid;
+          tasks.emplace_back([=, &bot_rec, &abort] {
+            if (!wait_count(bot_rec, (int)j + 1, abort) || !wait_event(X->ev_bot[j], abort)) return;
+            memcpy(eds_or_null + k * erowS + a, pin_bot + a, z - a);
+          });
+        }
+      }
+    }
+  }
+  X->pool->start(&tasks);
+
+  // device work, issued band by band as the staging lands
+  hipStream_t s = c->stream;
+  const char* fail = nullptr;
+  int frc = CDA_OK;
+  for (uint32_t b = 0; b < nband && !fail; b++) {
+    const size_t r0 = (size_t)b * kb;
+    while (staged[b].load(std::memory_order_acquire) > 0) std::this_thread::yield();  // the pool staged band b
+    if (hipMemcpyAsync(d_ods + r0 * rowS, src_in + r0 * rowS, band_b, hipMemcpyHostToDevice, c->h2d_stream) !=
+            hipSuccess ||
+        hipEventRecord(X->ev_in[b], c->h2d_stream) != hipSuccess || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
+      fail = "H2D";
+      break;
+    }
+    RsJob j = rows_job(k, 1, d_ods, d_eds);
+    j.src += r0 * rowS;
+    j.dst += r0 * erowS;
+    j.cpy += r0 * erowS;
+    j.cw_per_blk = (int)kb;
+    if (const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s)) {
+      frc = lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+      fail = "rows";
+      break;
+    }
+    if (want) {
+      uint8_t* dst = out_pinned ? eds_or_null + r0 * erowS + rowS : pin_q1 + r0 * rowS;
+      const size_t dpitch = out_pinned ? erowS : rowS;
+      if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
+          hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
+          hipMemcpy2DAsync(dst, dpitch, d_eds + r0 * erowS + rowS, erowS, rowS, kb, hipMemcpyDeviceToHost,
+                           c->d2h_stream) != hipSuccess ||
+          hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess) {
+        fail = "Q1 D2H";
+        break;
+      }
+      q1_rec.store((int)b + 1, std::memory_order_release);
+    }
+  }
+  if (!fail) {
+    const RsJob j = cols_job(k, 1, d_eds);
+    if (const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s)) {
+      frc = lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
+      fail = "cols";
+    }
+  }
+  if (!fail && want) {
+    if (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess)
+      fail = "event";
+    for (uint32_t j = 0; j < nchunk && !fail; j++) {
+      const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
+      uint8_t* dst = out_pinned ? eds_or_null + k * erowS + lo : pin_bot + lo;
+      if (hipMemcpyAsync(dst, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
+          hipEventRecord(X->ev_bot[j], c->d2h_stream) != hipSuccess) {
+        fail = "bottom D2H";
+        break;
+      }
+      bot_rec.store((int)j + 1, std::memory_order_release);
+    }
+  }
+  if (!fail) {
+    if ((rc = enqueue_commit(c, k, 1, d_eds, c->roots.p, c->dah.p, (unsigned long long*)c->status.p, s, 0))) {
+      frc = rc;
+      fail = "commit";
+    } else if (hipMemcpyAsync(X->pin_res, c->roots.p, roots_b, hipMemcpyDeviceToHost, s) != hipSuccess ||
+               hipMemcpyAsync(X->pin_res + roots_b, c->dah.p, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+               hipMemcpyAsync(X->pin_res + roots_b + 32, c->status.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+               hipEventRecord(X->ev_done, s) != hipSuccess) {
+      fail = "results D2H";
+    }
+  }
+  if (fail) abort.store(true);
+  X->pool->help_and_wait();
+  if (!fail) wait_event(X->ev_done, abort);
+  // every DMA of this call has finished before the caller's buffers (or the staging) can be touched again
+  const bool synced = hipStreamSynchronize(c->h2d_stream) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
+                      hipStreamSynchronize(c->d2h_stream) == hipSuccess;
+  if (fail) {
+    if (frc == CDA_OK) {
+      c->last_err = std::string("consensus path: ") + fail + ": " + hipGetErrorString(hipGetLastError());
+      frc = CDA_E_DEVICE;
+    }
+    return frc;
+  }
+  if (abort.load() || !synced) {
+    c->last_err = std::string("consensus path: ") + hipGetErrorString(hipGetLastError());
+    return CDA_E_DEVICE;
+  }
+  pack_roots(X->pin_res, w, row_roots);
+  pack_roots(X->pin_res + (size_t)w * CDA_REC_BYTES, w, col_roots);
+  memcpy(dah, X->pin_res + roots_b, 32);
+  uint64_t st;
+  memcpy(&st, X->pin_res + roots_b + 32, 8);
+  return map_status(st, 0, err);
+}
+
+}  // namespace cda

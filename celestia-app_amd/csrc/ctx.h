@@ -12,7 +12,8 @@
 #include "cda_internal.h"
 
 namespace cda {
-struct Stager;  // staging.cpp
+struct Stager;     // staging.cpp
+struct Consensus;  // consensus.cpp
 }
 
 struct cda_ctx {
@@ -66,6 +67,10 @@ struct cda_ctx {
   cda::Stager* st_in = nullptr;
   cda::Stager* st_out = nullptr;
   int staging = 3;
+  // the one-block host-buffer path (consensus.cpp): copy-thread pool, pinned slabs, events.  CDA_CONSENSUS=0 sends
+  // one-block calls down the serial form instead (A/B runs)
+  cda::Consensus* cons = nullptr;
+  bool consensus = true;
   // profiling
   bool prof = false;
   struct Pending {
@@ -118,6 +123,17 @@ int staged_h2d_runs(cda_ctx* c, void* d_dst, const uint8_t* h_base, const HostRu
                     hipStream_t s);
 void bind_helper_thread(const cda_ctx* c);  // the calling helper thread -> c->local_cpus (no-op if empty)
 void find_local_cpus(cda_ctx* c);
+// one block through host buffers, overlapped with pinned staging and a copy pool (consensus.cpp; lock held)
+bool consensus_eligible(const cda_ctx* c, uint32_t k);
+int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
+                    uint8_t* col_roots, uint8_t* dah, cda_err_info* err);
+void free_consensus(cda_ctx* c);
+// RS jobs of the block path: rows (ODS row r -> Q0 copy + Q1 row r) and columns (top half -> bottom half)
+RsJob rows_job(uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds);
+RsJob cols_job(uint32_t k, uint32_t nblocks, uint8_t* d_eds);
+// commitment phase (leaf hashing, NMT levels, DAH) of nblocks extended blocks in d_eds on stream s
+int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
+                   unsigned long long* d_status, hipStream_t s, size_t rec_off);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 // split_kernels.hip

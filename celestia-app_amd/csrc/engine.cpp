@@ -319,6 +319,7 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
   if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
   if (const char* e = getenv("CDA_STAGING")) c->staging = atoi(e) & 3;
+  if (const char* e = getenv("CDA_CONSENSUS")) c->consensus = atoi(e) != 0;
   find_local_cpus(c);
   // the streams that overlap each other, created right after `stream` so that they land on distinct hardware
   // queues (HIP assigns streams to its GPU_MAX_HW_QUEUES = 4 queues round-robin)
@@ -352,6 +353,7 @@ void cda_free(cda_ctx* c) {
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < cda_ctx::kJoin; i++)
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
+    free_consensus(c);  // joins its copy threads first
     free_pipeline(c);
     free_staging(c);
     if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
@@ -576,7 +578,9 @@ int cda_extend_commit_batch(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint
   if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
   Lock l(c);
   if (nblocks > 1 && !c->prof) return batch_pipelined(c, k, nblocks, ods, eds_or_null, row_roots, col_roots, dah, err, 0);
-  // one block (or profiling, where kernels must not overlap the event brackets): serial on c->stream
+  // one block: the consensus path's call (PrepareProposal / ProcessProposal), copies overlapped with the device work
+  if (nblocks == 1 && consensus_eligible(c, k)) return extend_one_host(c, k, ods, eds_or_null, row_roots, col_roots, dah, err);
+  // profiling (kernels must not overlap the event brackets) or k = 512: serial on c->stream
   const uint32_t w = 2 * k;
   const size_t ods_b = (size_t)nblocks * k * k * CDA_SHARE, eds_b = (size_t)nblocks * w * w * CDA_SHARE;
   const size_t roots_b = (size_t)nblocks * 2 * w * CDA_REC_BYTES;

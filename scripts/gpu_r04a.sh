@@ -1,8 +1,17 @@
 #!/bin/bash
-# round 4, first GPU pass: GF(2^16) tests after the compile-time diag-mode change, then the consensus-path probe.
+# round 4, first GPU pass: GF(2^16) + host-path tests, the consensus-path probe (serial form vs the new one-block
+# path), host first-touch rates, and short N=1 / N=2 benches with config C5's split.
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "512 or rs16 or ff16 or codec or abi" > gpurun_out/r04a_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "consensus or 512 or rs16 or ff16 or codec or abi or batch or fault" > gpurun_out/r04a_tests.log 2>&1
 rc=$?; tail -n 3 gpurun_out/r04a_tests.log; [ $rc -ne 0 ] && exit $rc
+CDA_CONSENSUS=0 timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04a_probe_serial.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/r04a_probe_serial.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04a_probe.log 2>&1
-rc=$?; cat gpurun_out/r04a_probe.log | grep -v amdgpu.ids; exit $rc
+rc=$?; grep -v amdgpu.ids gpurun_out/r04a_probe.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 ./tools/fault_probe > gpurun_out/r04a_fault.log 2>&1; cat gpurun_out/r04a_fault.log
+timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-extras --no-cpu-baseline > gpurun_out/r04a_bench1.log 2>&1
+rc=$?; grep '^{' gpurun_out/r04a_bench1.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("N1", d["value"], json.dumps(d.get("k512_split")))'; [ $rc -ne 0 ] && { tail -5 gpurun_out/r04a_bench1.log; exit $rc; }
+timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-extras --no-cpu-baseline > gpurun_out/r04a_bench2.log 2>&1
+rc=$?; grep '^{' gpurun_out/r04a_bench2.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("N2", d["value"], json.dumps(d.get("k512_split")))'; [ $rc -ne 0 ] && { tail -5 gpurun_out/r04a_bench2.log; exit $rc; }
+exit 0

@@ -1,0 +1,160 @@
+"""The one-block host-buffer path (csrc/consensus.cpp): cda_extend_commit / cda_extend_commit_batch with one block,
+as PrepareProposal / ProcessProposal call da.ExtendShares (app/prepare_proposal.go:65-93,
+app/process_proposal.go:137-151).  Row bands staged through pinned slabs by a copy pool, Q0 copied host to host,
+Q1 / the bottom half copied back while the device hashes.  Every case is bit-exact against the oracle, and against
+the serial form (a context opened with CDA_CONSENSUS=0) for the error reports."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def serial_ctx():
+    import os
+
+    import cda
+    old = os.environ.get("CDA_CONSENSUS")
+    os.environ["CDA_CONSENSUS"] = "0"
+    try:
+        c = cda.Context(0)
+    finally:
+        if old is None:
+            del os.environ["CDA_CONSENSUS"]
+        else:
+            os.environ["CDA_CONSENSUS"] = old
+    yield c
+    c.close()
+
+
+def _check(ods, eds, rr, cr, dah, want_eds=True):
+    rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods)
+    assert rc == 0
+    if want_eds:
+        assert np.array_equal(eds.reshape(eds_o.shape), eds_o), "EDS bytes differ"
+    assert np.array_equal(rr, rr_o) and np.array_equal(cr, cr_o), "roots differ"
+    assert bytes(dah) == dah_o
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128, 256])
+@pytest.mark.parametrize("want_eds", [True, False])
+def test_one_block_fresh_buffers(ctx, k, want_eds):
+    """cda_extend_commit with a fresh, never-touched EDS buffer (np.empty, as go/cda/extend.go allocates one)."""
+    ods = O.gen_ods(k, 0xC0DE + k)
+    eds, rr, cr, dah = ctx.extend_commit(ods.copy(), want_eds=want_eds)
+    _check(ods, eds, rr, cr, dah, want_eds)
+
+
+@pytest.mark.parametrize("k", [64, 128])
+def test_one_block_output_fully_overwritten(ctx, k):
+    """A reused output buffer full of other bytes: every byte of the EDS is written (Q0 by the host copy, Q1 and the
+    bottom half from the device)."""
+    ods = O.gen_ods(k, 0x5EED + k)
+    out = np.full((1, 4 * k * k, 512), 0xAB, np.uint8)
+    eds, rr, cr, dah = ctx.extend_commit_batch(ods[None], eds_out=out)
+    _check(ods, out[0], rr[0], cr[0], dah[0])
+
+
+@pytest.mark.parametrize("pin_in,pin_out", [(True, True), (True, False), (False, True)])
+def test_one_block_pinned_caller_buffers(ctx, pin_in, pin_out):
+    """Pinned caller memory (cda_host_alloc) takes the direct DMA, for the input, the output or both."""
+    k = 128
+    ods = O.gen_ods(k, 0x91 + 2 * pin_in + pin_out)
+    bufs = []
+    src = ods[None]
+    if pin_in:
+        p = ctx.pinned((1, k * k, 512))
+        p.array[:] = src
+        src = p.array
+        bufs.append(p)
+    out = None
+    if pin_out:
+        q = ctx.pinned((1, 4 * k * k, 512))
+        q.array[:] = 0x5A
+        out = q.array
+        bufs.append(q)
+    try:
+        eds, rr, cr, dah = ctx.extend_commit_batch(src, eds_out=out)
+        _check(ods, eds[0], rr[0], cr[0], dah[0])
+    finally:
+        for b in bufs:
+            b.free()
+
+
+def test_one_block_sizes_interleaved(ctx):
+    """Growing and shrinking k between calls (pinned slabs grow; smaller calls reuse them), with and without the
+    EDS: every call exact."""
+    for k, want in ((16, True), (256, False), (8, True), (256, True), (128, False), (32, True), (128, True)):
+        ods = O.gen_ods(k, 0x1234 + k + want)
+        eds, rr, cr, dah = ctx.extend_commit(ods, want_eds=want)
+        _check(ods, eds, rr, cr, dah, want)
+
+
+@pytest.mark.parametrize("k,swap,axis", [(128, (130, 131), 0), (64, None, 1), (8, (3, 5), 0)])
+def test_one_block_push_order_errors_match_serial(ctx, serial_ctx, k, swap, axis):
+    """Namespace push-order errors come back with the same axis / index / leaf as the serial form."""
+    import cda
+    ods = O.gen_ods(k, 0x77 + k).copy()
+    if swap is not None:
+        ods[list(swap)] = ods[list(swap[::-1])]
+    else:  # rows stay sorted, column 5 decreases between rows 9 and 10
+        sq = ods.reshape(k, k, 512)
+        sq[10, :, 19:29] = 0
+        sq[10, :, 29:] = 0
+        ods = np.sort(sq.view("S512").reshape(k, k), axis=1).view(np.uint8).reshape(k * k, 512)
+    errs = []
+    for c in (ctx, serial_ctx):
+        with pytest.raises(cda.CdaError) as ei:
+            c.extend_commit(ods)
+        e = ei.value
+        errs.append((e.code, e.axis, e.index, e.leaf))
+    assert errs[0] == errs[1] and errs[0][0] == -5 and errs[0][1] == axis
+
+
+def test_one_block_matches_serial_form(ctx, serial_ctx):
+    k = 128
+    ods = O.gen_ods(k, 0xABCD)
+    a = ctx.extend_commit(ods)
+    b = serial_ctx.extend_commit(ods)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
+
+
+def test_one_block_concurrent_callers(ctx):
+    """Several host threads on one context (the ctx lock serialises them; the copy pool is per context)."""
+    k = 64
+    odss = [O.gen_ods(k, 0x4000 + i) for i in range(6)]
+    want = [O.extend_commit(o)[4] for o in odss]
+    got = [None] * len(odss)
+
+    def run(i):
+        for _ in range(3):
+            got[i] = ctx.extend_commit(odss[i])[3]
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(odss))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert got == want
+
+
+def test_one_block_copy_pool_fault_is_a_return_code(monkeypatch):
+    """The copy pool's threads cannot start: CDA_E_INTERNAL, and the next call on the context works."""
+    import cda
+    from cda import _native as N
+    c = cda.Context(0)
+    try:
+        ods = O.gen_ods(32, 9)
+        monkeypatch.setenv("CDA_FAULT_INJECT", "thread")
+        with pytest.raises(cda.CdaError) as ei:
+            c.extend_commit(ods)
+        assert ei.value.code == N.E_INTERNAL
+        monkeypatch.delenv("CDA_FAULT_INJECT")
+        eds, rr, cr, dah = c.extend_commit(ods)
+        _check(ods, eds, rr, cr, dah)
+    finally:
+        c.close()
