@@ -220,4 +220,6 @@ struct cda_multi {
                                       // device copies instead of RCCL (tests, rehearsal of G > 1 on one GPU)
   std::mutex split_mu;                // one split at a time per handle
   cda::SplitComm* comm = nullptr;     // RCCL communicators (created by the first split with G > 1)
+  uint8_t* pin_res = nullptr;         // pinned: a split's roots, DAH and status words (one D2H per call)
+  size_t pin_cap = 0;
 };

@@ -292,6 +292,7 @@ int cda_multi_init(uint32_t device_mask, cda_multi** out) {
 void cda_multi_free(cda_multi* m) {
   if (!m) return;
   free_split_comm(m);
+  if (m->pin_res) (void)hipHostFree(m->pin_res);
   for (auto* c : m->ctx) cda_free(c);
   delete m;
 }

@@ -84,7 +84,9 @@ int ensure_split(cda_ctx* c, const Plan& p, int g) {
         (rc = ensure(c, c->sp_S, (size_t)p.G * p.rp * p.cp * (p.S + p.R))))
       return rc;
   }
-  if (g == 0 && (rc = ensure(c, c->sp_gather, ((size_t)p.G * p.meta_recs() + 4 * (size_t)p.k) * p.R + 64))) return rc;
+  // device 0: G meta arrays | 4k root records | DAH | G status words
+  if (g == 0 && (rc = ensure(c, c->sp_gather, ((size_t)p.G * p.meta_recs() + 4 * (size_t)p.k) * p.R + 32 + 8 * p.G)))
+    return rc;
   for (auto& e : c->sp_ev)
     if (!e && !dev_ok(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate")) return CDA_E_DEVICE;
   return CDA_OK;
@@ -406,10 +408,9 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
   if (G == 1) {
     // one device: its column slab is the whole 2k x 2k EDS, so the split is the block pipeline itself (RS rows and
     // columns, leaf hashing shared by row and column trees, all 4k trees, DAH) into the result area
-    uint8_t* gat = (uint8_t*)c0->sp_gather.p;
-    uint8_t* fin = gat + p.meta_recs() * p.R;
-    unsigned long long* st = (unsigned long long*)(gat + (p.meta_recs() - 1) * p.R);
-    HIPC(c0, hipMemsetAsync(st, 0xFF, 8, c0->stream), "memset");
+    // (the pipeline sets its status word itself; it sits behind the DAH, where the results copy reads it)
+    uint8_t* fin = (uint8_t*)c0->sp_gather.p + p.meta_recs() * p.R;
+    unsigned long long* st = (unsigned long long*)(fin + 4 * (size_t)k * p.R + 32);
     TRY(enqueue_pipeline(c0, k, 1, slab[0], (uint8_t*)c0->sp_C.p, fin, fin + 4 * (size_t)k * p.R, st, c0->stream));
   } else {
     for (uint32_t g = 0; g < G; g++) {
@@ -425,15 +426,26 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
     (void)hipSetDevice(c0->device);
     TRY(finish_pass(c0, p));
   }
-  // results: 4k roots + DAH + G status words from device 0; the EDS from where each part lives
+  // results: 4k roots + DAH + the G status words, gathered behind the DAH on device 0 and fetched by ONE copy into a
+  // pinned buffer of the handle; the EDS from where each part lives
   const size_t mr = p.meta_recs();
-  std::vector<uint8_t> fin(4 * (size_t)k * p.R + 32);
-  std::vector<uint64_t> st(G);
   uint8_t* gat = (uint8_t*)c0->sp_gather.p;
-  HIPC(c0, hipMemcpyAsync(fin.data(), gat + (size_t)G * mr * p.R, fin.size(), hipMemcpyDeviceToHost, c0->stream),
-       "D2H");
-  HIPC(c0, hipMemcpy2DAsync(st.data(), 8, gat + (mr - 1) * p.R, mr * p.R, 8, G, hipMemcpyDeviceToHost, c0->stream),
-       "D2H");
+  uint8_t* fin = gat + (size_t)G * mr * p.R;
+  const size_t res_b = 4 * (size_t)k * p.R + 32 + 8 * (size_t)G;
+  if (G > 1)
+    HIPC(c0, hipMemcpy2DAsync(fin + 4 * (size_t)k * p.R + 32, 8, gat + (mr - 1) * p.R, mr * p.R, 8, G,
+                              hipMemcpyDeviceToDevice, c0->stream),
+         "status");
+  if (m->pin_cap < res_b) {
+    if (m->pin_res) (void)hipHostFree(m->pin_res);
+    m->pin_res = nullptr;
+    m->pin_cap = 0;
+    (void)hipSetDevice(c0->device);
+    HIPC(c0, hipHostMalloc((void**)&m->pin_res, res_b, hipHostMallocDefault), "hipHostMalloc");
+    m->pin_cap = res_b;
+  }
+  (void)hipSetDevice(c0->device);
+  HIPC(c0, hipMemcpyAsync(m->pin_res, fin, res_b, hipMemcpyDeviceToHost, c0->stream), "D2H");
   if (eds && G == 1) {
     HIPC(c0, hipMemcpyAsync(eds, c0->sp_C.p, (size_t)p.w * p.w * p.S, hipMemcpyDeviceToHost, c0->stream), "D2H");
   } else if (eds) {
@@ -449,15 +461,23 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
            "D2H");
     }
   }
+  // device 0's stream ends after every device's part (the gather receives from all of them); the others are
+  // synchronised too so that the call returns with no work of it in flight
   for (uint32_t g = 0; g < G; g++) {
     (void)hipSetDevice(m->ctx[g]->device);
     HIPC(m->ctx[g], hipStreamSynchronize(m->ctx[g]->stream), "sync");
     flush_profile(m->ctx[g]);
   }
-  pack_roots(fin.data(), 2 * k, row_roots);
-  pack_roots(fin.data() + 2 * (size_t)k * p.R, 2 * k, col_roots);
-  memcpy(dah_out, fin.data() + 4 * (size_t)k * p.R, 32);
-  return map_status(*std::min_element(st.begin(), st.end()), -1, err);
+  pack_roots(m->pin_res, 2 * k, row_roots);
+  pack_roots(m->pin_res + 2 * (size_t)k * p.R, 2 * k, col_roots);
+  memcpy(dah_out, m->pin_res + 4 * (size_t)k * p.R, 32);
+  uint64_t st = ~0ull;
+  for (uint32_t g = 0; g < G; g++) {
+    uint64_t v;
+    memcpy(&v, m->pin_res + 4 * (size_t)k * p.R + 32 + 8 * (size_t)g, 8);
+    st = std::min(st, v);
+  }
+  return map_status(st, -1, err);
 }
 
 int check_split_args(cda_multi* m, uint32_t k, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah) {

@@ -3,7 +3,7 @@
 # path), host first-touch rates, and short N=1 / N=2 benches with config C5's split.
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "consensus or 512 or rs16 or ff16 or codec or abi or batch or fault" > gpurun_out/r04a_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "consensus or split or 512 or rs16 or ff16 or codec or abi or batch or fault" > gpurun_out/r04a_tests.log 2>&1
 rc=$?; tail -n 3 gpurun_out/r04a_tests.log; [ $rc -ne 0 ] && exit $rc
 CDA_CONSENSUS=0 timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04a_probe_serial.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/r04a_probe_serial.log; [ $rc -ne 0 ] && exit $rc
