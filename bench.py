@@ -343,27 +343,50 @@ def pmc_counters(kernel, B):
     """Per-launch PMC values of `kernel` from the newest committed rocprofv3 summary
     (profiles/r0*_counters.json; scripts/profile.sh + scripts/summarize_prof.py), scaled from the
     profiled batch to B.  hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (the gfx950 correction of
-    MI355X_MICROARCH.md); valu_insts = SQ_INSTS_VALU (wave-instructions).  None if not covered."""
+    MI355X_MICROARCH.md); valu_insts = SQ_INSTS_VALU (wave-instructions).  The NMT levels kernel runs
+    with several grid sizes per step; summaries from round 4 on split its dispatches by grid
+    ("nmt_levels_kernel@grid=N"): the largest grid is levels 1-2 (nmt_levels_1), the others the upper
+    levels (nmt_levels, averaged per launch).  None if not covered."""
     import glob
-    if kernel not in PMC_NAMES:
-        return None
     import re
 
     def order(f):  # r<round>_v<version>_counters.json, newest last
         m = re.match(r"r(\d+)(?:_v(\d+))?", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2) or 0)) if m else (0, 0)
+
+    def per_grid(d, name):
+        g = [(int(k.split("@grid=")[1]), v) for k, v in d.items() if k.startswith(name + "@grid=")]
+        return sorted(g, key=lambda x: -x[0])
+
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_counters.json")), key=order)
     for f in reversed(files):
         try:
-            c = json.load(open(f)).get(PMC_NAMES[kernel])
+            d = json.load(open(f))
         except (OSError, ValueError):
             continue
+        if kernel in PMC_NAMES:
+            c, src = d.get(PMC_NAMES[kernel]), PMC_NAMES[kernel]
+        elif kernel in ("nmt_levels_1", "nmt_levels"):
+            g = per_grid(d, "nmt_levels_kernel")
+            if len(g) < 2:
+                continue
+            if kernel == "nmt_levels_1":
+                c, src = g[0][1], f"nmt_levels_kernel@grid={g[0][0]}"
+            else:
+                rest = [v for _, v in g[1:]]
+                n = sum(v.get("dispatches", 1) for v in rest)
+                c = {key: sum(v.get(key, 0) * v.get("dispatches", 1) for v in rest) / n
+                     for key in ("hbm_bytes_corrected", "SQ_INSTS_VALU") if all(key in v for v in rest)}
+                c["bench_batch"] = rest[0].get("bench_batch", PMC_BATCH)
+                src = "nmt_levels_kernel@grid<" + str(g[0][0])
+        else:
+            return None
         if not c:
             continue
         scale = B / float(c.get("bench_batch", PMC_BATCH))
         return {"hbm_bytes": int(c["hbm_bytes_corrected"] * scale) if "hbm_bytes_corrected" in c else None,
                 "valu_insts": c["SQ_INSTS_VALU"] * scale if "SQ_INSTS_VALU" in c else None,
-                "source": f"{os.path.relpath(f, ROOT)} ({PMC_NAMES[kernel]}, B={c.get('bench_batch', PMC_BATCH)} "
+                "source": f"{os.path.relpath(f, ROOT)} ({src}, B={c.get('bench_batch', PMC_BATCH)} "
                           f"profile scaled to B={B})"}
     return None
 

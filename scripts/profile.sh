@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/prof
 TAG=${1:-r01}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras ${BENCH_ARGS:-}"
+BENCH="$R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras --no-k512-split ${BENCH_ARGS:-}"
 step() {  # name timeout args...
   local name=$1 t=$2; shift 2
   echo "== $name"

@@ -23,16 +23,37 @@ def short(n):
     n = n.replace("HIP_vector_type<unsigned int, 4u>", "uint4")
     return n.split("(")[0].replace("cda::", "").replace("void ", "")
 
+def grid(r):
+    """Total work-items of a dispatch (rocprofv3 writes Grid_Size, or Grid_Size_X/Y/Z)."""
+    if r.get("Grid_Size"):
+        return int(r["Grid_Size"])
+    g = 1
+    for a in "XYZ":
+        g *= int(r.get(f"Grid_Size_{a}") or 1)
+    return g
+
+
+# per kernel name, and per (name, grid size) when one kernel is dispatched with several grid sizes (the NMT levels
+# kernel: levels 1-2 over every tree, then the thinner upper levels) -- "<name>@grid=<n>"
 counters = collections.defaultdict(lambda: collections.defaultdict(list))
 durations = collections.defaultdict(list)
+grids = collections.defaultdict(set)
 for sub in sorted(os.listdir(src)):
     p = os.path.join(src, sub, "run_counter_collection.csv")
     if not os.path.exists(p):
         continue
     for r in csv.DictReader(open(p)):
-        counters[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        n = short(r["Kernel_Name"])
+        counters[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        counters[f"{n}@grid={grid(r)}"][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        grids[n].add(grid(r))
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
-    durations[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    n = short(r["Kernel_Name"])
+    durations[n].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    durations[f"{n}@grid={grid(r)}"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+for n, gs in grids.items():  # single-grid kernels need no per-grid entries
+    if len(gs) == 1:
+        counters.pop(f"{n}@grid={next(iter(gs))}", None)
 
 summary = {}
 for k, cs in counters.items():

@@ -5,8 +5,11 @@
  * include/cda.h); run by tests/test_abi_client.py on the GPU, which checks its outputs against
  * tests/golden/oracle_digests.json and mainnet block 408's data_hash.
  *
- *   abi_host_client <ods.bin> <k> <out_dir>
+ *   abi_host_client <ods.bin> <k> <out_dir> [<blobs.bin>]
  * writes <out_dir>/{eds,row_roots,col_roots,dah,parity,repaired,commitments}.bin and prints one status line.
+ * With <blobs.bin> ([u32 n][n x 29-B namespace][(n + 1) x u64 data offsets][data]) it also computes the share
+ * commitments of all n blobs in ONE cda_blob_commitments call -- ProcessProposal's pre-pass over every BlobTx of a
+ * proposal (go/patches/0003) -- into <out_dir>/proposal_commitments.bin.
  * Also checked in-process: Codec.Decode of an erased row, a wrapper tree root, the multi-device batch.
  */
 #include <stdint.h>
@@ -33,8 +36,8 @@ static int fail(const char* what, int rc, const cda_err_info* e) {
 }
 
 int main(int argc, char** argv) {
-  if (argc != 4) {
-    fprintf(stderr, "usage: %s <ods.bin> <k> <out_dir>\n", argv[0]);
+  if (argc != 4 && argc != 5) {
+    fprintf(stderr, "usage: %s <ods.bin> <k> <out_dir> [<blobs.bin>]\n", argv[0]);
     return 2;
   }
   const uint32_t k = (uint32_t)atoi(argv[2]), w = 2 * k, count = k * k;
@@ -132,6 +135,36 @@ int main(int argc, char** argv) {
   uint8_t commitments[64];
   rc = cda_blob_commitments(ctx, 2, ns2, ods, offs, NULL, 64, commitments, &err);
   if (rc) return fail("cda_blob_commitments", rc, &err);
+
+  /* ProcessProposal's pre-pass: every blob of a proposal in one call */
+  if (argc == 5) {
+    FILE* bf = fopen(argv[4], "rb");
+    if (!bf || fseek(bf, 0, SEEK_END) != 0) {
+      fprintf(stderr, "cannot read %s\n", argv[4]);
+      return 2;
+    }
+    const long bsz = ftell(bf);
+    uint8_t* bb = malloc((size_t)bsz + 1);
+    rewind(bf);
+    if (bsz < 4 || fread(bb, 1, (size_t)bsz, bf) != (size_t)bsz) {
+      fprintf(stderr, "cannot read %s\n", argv[4]);
+      return 2;
+    }
+    fclose(bf);
+    uint32_t nb;
+    memcpy(&nb, bb, 4);
+    const uint8_t* bns = bb + 4;
+    uint64_t* boffs = malloc(((size_t)nb + 1) * 8);
+    memcpy(boffs, bns + (size_t)nb * CDA_NAMESPACE_SIZE, ((size_t)nb + 1) * 8);
+    const uint8_t* bdata = bns + (size_t)nb * CDA_NAMESPACE_SIZE + ((size_t)nb + 1) * 8;
+    uint8_t* pc = malloc((size_t)nb * 32);
+    rc = cda_blob_commitments(ctx, nb, bns, bdata, boffs, NULL, 64, pc, &err);
+    if (rc) return fail("cda_blob_commitments (proposal)", rc, &err);
+    if (write_file(argv[3], "proposal_commitments.bin", pc, (size_t)nb * 32)) return 1;
+    free(pc);
+    free(boffs);
+    free(bb);
+  }
 
   /* the multi-device handle over every visible GPU: two blocks, same DAH each */
   cda_multi* multi = NULL;

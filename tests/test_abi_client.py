@@ -20,10 +20,18 @@ def test_client_is_built():
     assert os.path.exists(CLIENT), "run __graft_entry__.build() (make -C tests/abi_client)"
 
 
-def _run(tmp_path, ods, k):
+def _run(tmp_path, ods, k, blobs=None):
     src = tmp_path / "ods.bin"
     src.write_bytes(np.ascontiguousarray(ods, np.uint8).tobytes())
-    out = subprocess.run([CLIENT, str(src), str(k), str(tmp_path)], capture_output=True, text=True, timeout=180)
+    extra = []
+    if blobs is not None:  # [(ns29, data)] -> blobs.bin ([u32 n][n x 29][(n + 1) x u64][data])
+        offs = np.zeros(len(blobs) + 1, np.uint64)
+        offs[1:] = np.cumsum([len(d) for _, d in blobs])
+        (tmp_path / "blobs.bin").write_bytes(np.uint32(len(blobs)).tobytes() + b"".join(n for n, _ in blobs) +
+                                             offs.tobytes() + b"".join(d for _, d in blobs))
+        extra = [str(tmp_path / "blobs.bin")]
+    out = subprocess.run([CLIENT, str(src), str(k), str(tmp_path)] + extra, capture_output=True, text=True,
+                         timeout=180)
     assert out.returncode == 0, out.stderr
     assert "abi_host_client ok" in out.stdout
     rd = lambda n: (tmp_path / n).read_bytes()  # noqa: E731
@@ -50,7 +58,20 @@ def test_abi_client_matches_golden_digests(tmp_path, k):
 
 @pytest.mark.gpu
 def test_abi_client_mainnet_block_408(tmp_path):
+    """Block 408 through the C ABI: the DAH is the header's data_hash, and the proposal pre-pass (one
+    cda_blob_commitments call over block 408's blob plus synthetic blobs, as ProcessProposal batches every BlobTx)
+    reproduces the commitment the block's MsgPayForBlobs carries and the oracle's for the others."""
     z = np.load(os.path.join(HERE, "golden", "mainnet_h408.npz"))
-    eds, rr, cr, dah, repaired = _run(tmp_path, z["ods"], 32)
+    b = np.load(os.path.join(HERE, "golden", "mainnet_h408_blobs.npz"))
+    rng = np.random.default_rng(408)
+    blobs = [(b["namespaces"][0].tobytes(), b["data"].tobytes())]
+    for n in (1, 511, 4000, 70000):
+        blobs.append((bytes(19) + bytes([n % 251 + 1]) + bytes(rng.integers(0, 256, 9, dtype=np.uint8)),
+                      bytes(rng.integers(0, 256, n, dtype=np.uint8))))
+    eds, rr, cr, dah, repaired = _run(tmp_path, z["ods"], 32, blobs)
     assert dah == z["data_hash"].tobytes()
     assert repaired == eds
+    got = (tmp_path / "proposal_commitments.bin").read_bytes()
+    assert got[:32] == b["commitments"][0].tobytes()  # the PFB's share commitment in mainnet block 408
+    for i, (ns, d) in enumerate(blobs):
+        assert got[32 * i:32 * (i + 1)] == O.blob_commitment(ns, d)[1], i
