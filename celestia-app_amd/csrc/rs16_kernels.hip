@@ -585,20 +585,266 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int w) {
   }
 }
 
+#ifndef CDA_RS16_PIPE
+#define CDA_RS16_PIPE 1  // 0: the round-3 loop (body), for same-box A/B builds
+#endif
+
+// 64-B unit of one position: raw 16-B chunks <-> the 16 plane words of the state
+__device__ __forceinline__ void to_state(const uint4& q0, const uint4& q1, const uint4& q2, const uint4& q3, uint32_t m1,
+                                         const SliceMasks& km, uint32_t (&Er)[16]) {
+  uint32_t lo[8], hi[8];
+  pair_in(q0, q1, q2, q3, m1, lo, hi);
+  bitslice8(lo, km);
+  bitslice8(hi, km);
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    Er[j] = lo[j];
+    Er[8 + j] = hi[j];
+  }
+  change_basis<false>(Er);
+}
+__device__ __forceinline__ void from_state(const uint32_t (&Er)[16], uint32_t m1, const SliceMasks& ko, uint4& q0,
+                                           uint4& q1, uint4& q2, uint4& q3) {
+  uint32_t v[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) v[j] = Er[j];
+  change_basis<true>(v);
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    lo[j] = v[j];
+    hi[j] = v[8 + j];
+  }
+  bitslice8(lo, ko);
+  bitslice8(hi, ko);
+  pair_out(lo, hi, m1, q0, q1, q2, q3);
+}
+
+// The LDS prefetch of positions r = 0, 1, all in inline asm.  hipcc waits vmcnt(0) -- the whole store drain -- at
+// the first use of any load result and before any barrier while it knows of an LDS-DMA in flight, and treats an
+// LDS read after one the same way; loads, stores and LDS-DMA in fact retire from vmcnt in issue order
+// (MI355X_MICROARCH.md, s_waitcnt).  So the DMA is issued by asm (the compiler sees no LDS-DMA) and read back by asm
+// behind a counted wait: exactly kAfterPrefetch vector-memory instructions of this wave follow the 8 DMA loads in
+// program order (the 16 parity stores and the 8 loads of r = 2, 3 of the store phase), so vmcnt(24) is the wait
+// for the prefetch alone.  The compiler's own waits for the r = 2, 3 loads then stay partial.
+constexpr int kAfterPrefetch = 24;  // in the loop; 8 (the R loads) after the prologue's prefetch
+// M0 is reserved by the compiler; nothing else in this kernel uses it (the only M0 writes in its ISA are these), and
+// the clobber still tells the compiler it changes.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16(const uint8_t* g, uint32_t lds_uniform) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "s"(lds_uniform) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+// 8 DMA loads: position r (0, 1), chunk q (0..3) of this wave's share -> slot (r * 4 + q) of xw (lane-linear)
+__device__ __forceinline__ void prefetch01(const uint8_t* src, long long sh, int pl, const uint4* xw) {
+  const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr)xw);
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const uint8_t* sp = src + (pl + r) * sh;  // pos_r(LA, r) = r for r < 2 (LA: p0 -> R0)
+#pragma unroll
+    for (int q = 0; q < 4; q++) glds16(sp + 128 * q, base + (uint32_t)(r * 4 + q) * 1024u);
+  }
+}
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 u4(v4u v) { return make_uint4(v.x, v.y, v.z, v.w); }
+template <int N>
+__device__ __forceinline__ void read_prefetch(const uint4* xl, uint4 (&q)[2][4]) {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx9");
+  const uint32_t addr = (uint32_t)(uintptr_t)(lds_ptr)xl;
+  v4u a0, a1, a2, a3, a4, a5, a6, a7;
+  asm volatile(
+      "s_waitcnt vmcnt(%9)\n\t"
+      "ds_read_b128 %0, %8\n\t"
+      "ds_read_b128 %1, %8 offset:1024\n\t"
+      "ds_read_b128 %2, %8 offset:2048\n\t"
+      "ds_read_b128 %3, %8 offset:3072\n\t"
+      "ds_read_b128 %4, %8 offset:4096\n\t"
+      "ds_read_b128 %5, %8 offset:5120\n\t"
+      "ds_read_b128 %6, %8 offset:6144\n\t"
+      "ds_read_b128 %7, %8 offset:7168\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(a4), "=&v"(a5), "=&v"(a6), "=&v"(a7)
+      : "v"(addr), "i"(N)
+      : "memory");
+  q[0][0] = u4(a0), q[0][1] = u4(a1), q[0][2] = u4(a2), q[0][3] = u4(a3);
+  q[1][0] = u4(a4), q[1][1] = u4(a5), q[1][2] = u4(a6), q[1][3] = u4(a7);
+}
+
+__device__ __forceinline__ int lane_id() {  // recomputed where needed: a loop-carried copy was spilled to scratch,
+                                             // and the reload's vmcnt(0) waited for the whole store drain
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// Top of codeword g: r = 0, 1 from the LDS prefetch (N = the vector-memory instructions issued after it), layer 0's
+// (0, 1) butterfly, then r = 2, 3 from R and layer 0's (2, 3) butterfly.  (The Q0 copy of the rows pass stores the
+// raw chunks on the way.)  Instantiated twice -- after the prologue and at the end of the loop body -- so that the
+// compiler's wait for R in each copy is computed from one straight-line history, not merged at a loop header.
+template <int OM, int N>
+__device__ __forceinline__ void top_part(const Args& a, uint4* xw, int w, int g, const Ctx& cx, uint4 (&R)[2][4],
+                                         uint32_t (&E)[4][16]) {
+  const int lane = lane_id();
+  const int u = lane & 7;
+  const int pl = pos_lane(LA, lane) + pos_wave(LA, w);
+  const SliceMasks km = slice_masks();
+  uint32_t m1 = (lane & 2) ? ~0u : 0u;
+  asm volatile("" : "+v"(m1));
+  const int slice = g % a.slices;
+  const int cw = (g / a.slices) % a.cw_per_blk, blk = (g / a.slices) / a.cw_per_blk;
+  uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + (long long)slice * 512 + u * 16 : nullptr;
+  {
+    uint4 q[2][4];
+    read_prefetch<N>(xw + lane, q);
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      if (cpy) {
+        uint4* o = reinterpret_cast<uint4*>(cpy + (pl + pos_r(LA, r)) * a.cpy_sh);
+        o[0] = q[r][0], o[8] = q[r][1], o[16] = q[r][2], o[24] = q[r][3];
+      }
+      to_state(q[r][0], q[r][1], q[r][2], q[r][3], m1, km, E[r]);
+    }
+  }
+  butterfly<LA, true, 0, 0, OM>(E, cx);  // layer 0, pair (0, 1): before r = 2, 3 are needed
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 2; r < 4; r++) {
+    if (cpy) {
+      uint4* o = reinterpret_cast<uint4*>(cpy + (pl + pos_r(LA, r)) * a.cpy_sh);
+      o[0] = R[r - 2][0], o[8] = R[r - 2][1], o[16] = R[r - 2][2], o[24] = R[r - 2][3];
+    }
+    to_state(R[r - 2][0], R[r - 2][1], R[r - 2][2], R[r - 2][3], m1, km, E[r]);
+  }
+  butterfly<LA, true, 0, 2, OM>(E, cx);
+}
+
+// Software-pipelined persistent loop (round 4).  Per codeword g of this workgroup:
+//   top      (top_part) r = 0, 1 from the LDS prefetch; layer 0's (0, 1) butterfly; r = 2, 3 from the registers R
+//            that the previous store phase loaded; layer 0's (2, 3) butterfly.
+//   middle   the transforms as in body(); after the last exchange, global_load_lds of r = 0, 1 of codeword g + grid.
+//   bottom   r = 2: parity stores, then the NEXT codeword's r = 2 loads into R[0] (the registers E[2] just freed);
+//            r = 3 likewise into R[1]; then the r = 0, 1 stores.
+// On gfx950 vmcnt counts loads and stores in one in-order counter, so in body() the next codeword's direct loads,
+// issued after all 16 stores, could not be waited for without draining every store first.  Here the waits are
+// (a) vmcnt(24) for the LDS prefetch: nothing of the store phase; (b) the compiler's wait before R[0] is first read:
+// the r = 2, 3 stores and loads only, while the r = 0, 1 stores still drain -- and that wait comes after the
+// conversion of r = 0, 1 and a per-lane butterfly.  No extra registers: each load lands in the 16 VGPRs its
+// position's state just left.  Without a next codeword the loads read the first 512 B of the source (cache hits)
+// instead of re-reading a whole codeword.
+template <int OM>
+__device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
+  const int lane0 = threadIdx.x & 63;
+  Ctx cx{a.cpoly, lane0, w, {}, ((lane0 >> 3) & 1) ? ~0u : 0u};
+  asm volatile("" : "+v"(cx.lm3));
+  lv_fetch_all(cx);
+  uint4* xw = xb + w * 512;  // this wave's prefetch slots [r = 0, 1][q = 0..3][lane]
+  uint4 R[2][4];             // positions r = 2, 3 of the next codeword, raw
+  int g = blockIdx.x;
+  {  // prologue: the first codeword's r = 0, 1 into the LDS slots, r = 2, 3 into R (the loop's own order)
+    const int u = lane0 & 7;
+    const int pl = pos_lane(LA, lane0) + pos_wave(LA, w);
+    const int slice = g % a.slices;
+    const int cw = (g / a.slices) % a.cw_per_blk, blk = (g / a.slices) / a.cw_per_blk;
+    const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + (long long)slice * 512 + u * 16;
+    prefetch01(src, a.src_sh, pl, xw);
+#pragma unroll
+    for (int r = 2; r < 4; r++) {
+      const uint4* p = reinterpret_cast<const uint4*>(src + (pl + pos_r(LA, r)) * a.src_sh);
+      R[r - 2][0] = p[0], R[r - 2][1] = p[8], R[r - 2][2] = p[16], R[r - 2][3] = p[24];
+    }
+  }
+  uint32_t E[4][16];
+  top_part<OM, 8>(a, xw, w, g, cx, R, E);  // after the prologue only its 8 R loads follow the prefetch
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(cx.lv[i]));
+    asm volatile("" : "+v"(cx.lm3));
+    const int lane = lane_id();
+    const int u = lane & 7;
+    const int pl = pos_lane(LA, lane) + pos_wave(LA, w);
+    const int gn = g + (int)gridDim.x;
+    const bool more = gn < a.total;
+    // the next codeword's source (a dummy 512-B window of the source when there is none)
+    const int gq = more ? gn : 0;
+    const int sln = gq % a.slices;
+    const int cwn = (gq / a.slices) % a.cw_per_blk, bn = (gq / a.slices) / a.cw_per_blk;
+    const uint8_t* srcn = a.src + bn * a.src_blk + cwn * a.src_cw + (long long)sln * 512 + u * 16;
+    const long long shn = more ? a.src_sh : 0;
+    // IFFT, D = 1 .. m/2
+    layer<LA, true, 1, OM>(E, cx);
+    swap_lane45(E);
+    layer<LB, true, 2, OM>(E, cx);
+    swap_lane3(E, cx.lm3);
+    layer<LC, true, 3, OM>(E, cx);
+    layer<LC, true, 4, OM>(E, cx);
+    __syncthreads();  // every wave has read its prefetch slots before the exchange overwrites them
+    exchange_w<0>(E, xb, w, lane);
+    layer<LD, true, 5, OM>(E, cx);
+    layer<LD, true, 6, OM>(E, cx);
+    exchange_w<1>(E, xb, w, lane);
+    layer<LE, true, 7, OM>(E, cx);
+    layer<LE, true, 8, OM>(E, cx);
+    // FFT, D = m/2 .. 1
+    layer<LE, false, 8, OM>(E, cx);
+    layer<LE, false, 7, OM>(E, cx);
+    exchange_w<1>(E, xb, w, lane);
+    layer<LD, false, 6, OM>(E, cx);
+    layer<LD, false, 5, OM>(E, cx);
+    exchange_w<0>(E, xb, w, lane);  // ends with a barrier: the exchange buffer is free until the next codeword
+    prefetch01(srcn, shn, pl, xw);
+    layer<LC, false, 4, OM>(E, cx);
+    layer<LC, false, 3, OM>(E, cx);
+    swap_lane3(E, cx.lm3);
+    layer<LB, false, 2, OM>(E, cx);
+    swap_lane45(E);
+    layer<LA, false, 1, OM>(E, cx);
+    layer<LA, false, 0, OM>(E, cx);
+    {  // parity shard s = point s; r = 2, 3 first, each followed by the next codeword's loads of that position
+      uint32_t m1 = (lane & 2) ? ~0u : 0u;
+      asm volatile("" : "+v"(m1));
+      const int slice = g % a.slices;
+      const int cw = (g / a.slices) % a.cw_per_blk, blk = (g / a.slices) / a.cw_per_blk;
+      uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + (long long)slice * 512 + u * 16;
+      const SliceMasks ko = slice_masks();
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int r = (i + 2) & 3;
+        uint4 q0, q1, q2, q3;
+        from_state(E[r], m1, ko, q0, q1, q2, q3);
+        uint4* o = reinterpret_cast<uint4*>(dst + (pl + pos_r(LA, r)) * a.dst_sh);
+        o[0] = q0, o[8] = q1, o[16] = q2, o[24] = q3;
+        if (r >= 2) {
+          const uint4* p = reinterpret_cast<const uint4*>(srcn + (pl + pos_r(LA, r)) * shn);
+          R[r - 2][0] = p[0], R[r - 2][1] = p[8], R[r - 2][2] = p[16], R[r - 2][3] = p[24];
+        }
+      }
+    }
+    if (!more) break;
+    g = gn;
+    top_part<OM, kAfterPrefetch>(a, xw, w, g, cx, R, E);
+  }
+}
+
 // one whole body per value of W1..W3 (scalar branch at entry; each runs to the end, so no control-flow merge with
 // the 64 live state registers follows the specialised layers -- such a merge made the register allocator spill)
 __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if CDA_RS16_PIPE && CDA_RS16_DIAG_MODE == 0
+#define CDA_RS16_BODY body2
+#else
+#define CDA_RS16_BODY body
+#endif
   switch (w >> 1) {
-    case 0: body<0>(a, xb, w); break;
-    case 1: body<1>(a, xb, w); break;
-    case 2: body<2>(a, xb, w); break;
-    case 3: body<3>(a, xb, w); break;
-    case 4: body<4>(a, xb, w); break;
-    case 5: body<5>(a, xb, w); break;
-    case 6: body<6>(a, xb, w); break;
-    default: body<7>(a, xb, w); break;
+    case 0: CDA_RS16_BODY<0>(a, xb, w); break;
+    case 1: CDA_RS16_BODY<1>(a, xb, w); break;
+    case 2: CDA_RS16_BODY<2>(a, xb, w); break;
+    case 3: CDA_RS16_BODY<3>(a, xb, w); break;
+    case 4: CDA_RS16_BODY<4>(a, xb, w); break;
+    case 5: CDA_RS16_BODY<5>(a, xb, w); break;
+    case 6: CDA_RS16_BODY<6>(a, xb, w); break;
+    default: CDA_RS16_BODY<7>(a, xb, w); break;
   }
 }
 

@@ -1,9 +1,12 @@
 #!/bin/bash
-# round 4, first GPU pass: GF(2^16) + host-path tests, the consensus-path probe (serial form vs the new one-block
-# path), host first-touch rates, and short N=1 / N=2 benches with config C5's split.
+# round 4, first GPU pass: the GF(2^16) encoder rework (parity + A/B vs the round-3 loop), host-path / consensus /
+# proposal / split tests, the consensus-path probe (serial form vs the new one-block path), host first-touch rates,
+# and short N=1 / N=2 benches with config C5's split.
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "consensus or split or 512 or rs16 or ff16 or codec or abi or batch or fault" > gpurun_out/r04a_tests.log 2>&1
+timeout -k 10 900 bash scripts/gpu_rs16_ab.sh celestia-app_amd/cda/libcda.so ab/libcda_pipe0.so > gpurun_out/r04a_rs16.log 2>&1
+rc=$?; cat gpurun_out/r04a_rs16.log | grep -v amdgpu.ids | tail -8; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "consensus or proposal or abi_client or batch or fault or mainnet" > gpurun_out/r04a_tests.log 2>&1
 rc=$?; tail -n 3 gpurun_out/r04a_tests.log; [ $rc -ne 0 ] && exit $rc
 CDA_CONSENSUS=0 timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04a_probe_serial.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/r04a_probe_serial.log; [ $rc -ne 0 ] && exit $rc
