@@ -227,10 +227,14 @@ bool wait_event(hipEvent_t e, std::atomic<bool>& abort) {
   }
 }
 
-void touch_pages(uint8_t* p, size_t n) {  // first-touch a range of the caller's output (zero bytes: overwritten later)
-  volatile uint8_t* v = p;
-  for (size_t o = 0; o < n; o += 4096) v[o] = 0;
-  if (n) v[n - 1] = 0;
+// First touch of a range of the caller's output while the device works.  A locked OR with 0 per page: it takes the
+// page fault with write intent (the kernel maps a fresh page once, no zero-page / copy-on-write detour) and leaves
+// whatever is there -- a copy task of the same page may already have written it on another thread.
+// (asm: the compiler lowers an idempotent atomic RMW to a plain load, which only maps the shared zero page.)
+inline void touch_byte(uint8_t* b) { asm volatile("lock orb $0, %0" : "+m"(*b) : : "memory"); }
+void touch_pages(uint8_t* p, size_t n) {
+  for (size_t o = 0; o < n; o += 4096) touch_byte(p + o);
+  if (n) touch_byte(p + n - 1);
 }
 
 }  // namespace
