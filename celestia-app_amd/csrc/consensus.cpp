@@ -266,7 +266,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   // bands of the row pass (an even number of rows each: the FF8 encoder takes codeword pairs) and chunks of the
   // bottom half's copy-out
   const uint32_t nband = k >= 16 ? 4 : 1, kb = k / nband;
-  const uint32_t nchunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, bot_b >> 20));
+  const uint32_t nchunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(Consensus::kMaxChunks, bot_b >> 20));
   const uint8_t* src_in = in_pinned ? ods : X->pin_in;
   uint8_t* d_ods = (uint8_t*)c->ods.p;
   uint8_t* d_eds = (uint8_t*)c->eds.p;
@@ -314,10 +314,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
             for (uint32_t r = r0; r < std::min((b + 1) * kb, r0 + rows_per_task); r++)
               memcpy(eds_or_null + r * erowS + rowS, pin_q1 + r * rowS, rowS);
           });
-      for (uint32_t j = 0; j < nchunk; j++) {  // bottom-half chunk j, two tasks each
-        const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk, mid = (lo + hi) / 2;
-        for (int h = 0; h < 2; h++) {
-          const size_t a = h ? mid : lo, z = h ? hi : mid;
+      for (uint32_t j = 0; j < nchunk; j++) {  // bottom-half chunk j (1 MiB at k = 128), four tasks each: the last
+                                               // chunk's host copy is on the critical path
+        const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
+        for (int h = 0; h < 4; h++) {
+          const size_t a = lo + (hi - lo) * h / 4, z = lo + (hi - lo) * (h + 1) / 4;
           tasks.emplace_back([=, &bot_rec, &abort] {
             if (!wait_count(bot_rec, (int)j + 1, abort) || !wait_event(X->ev_bot[j], abort)) return;
             memcpy(eds_or_null + k * erowS + a, pin_bot + a, z - a);

@@ -48,12 +48,21 @@ def series(want_eds, fresh_out):
     return {"min": round(min(out), 3), "median": round(float(np.median(out)), 3), "max": round(max(out), 3)}
 
 
-res = {"reps": reps}
+res = {"reps": reps, "consensus": os.environ.get("CDA_CONSENSUS", "1")}
 res["fresh_with_eds"] = series(True, True)
 res["fresh_roots_only"] = series(False, True)
 res["reused_with_eds"] = series(True, False)
 res["reused_roots_only"] = series(False, False)
 print(json.dumps(res), flush=True)
+if os.environ.get("CDA_CONSENSUS", "1") != "0":  # copy-pool size sweep (a context reads CDA_COPY_THREADS at its first call)
+    sweep = {}
+    for T in (3, 7, 11, 15):
+        os.environ["CDA_COPY_THREADS"] = str(T)
+        ctx.close()
+        ctx = cda.Context(0)
+        sweep[str(T)] = series(True, True)
+    os.environ.pop("CDA_COPY_THREADS")
+    print(json.dumps({"copy_threads_sweep_fresh_with_eds": sweep}), flush=True)
 
 # host side: first-touch copies into fresh pages
 N = 32 << 20
