@@ -16,6 +16,12 @@ for i in 1 2 3; do
     echo "c2 $lib $(CDA_LIB=$lib timeout -k 10 120 python scripts/c2_probe.py 2>/dev/null)" || exit 1
   done
 done
+for i in 1 2; do
+  for m in 0 4 8; do
+    CDA_MIXED=$m timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-extras --no-cpu-baseline --no-k512-split > gpurun_out/r04a_mixed.log 2>&1 || { tail -5 gpurun_out/r04a_mixed.log; exit 1; }
+    echo "mixed=$m $(grep '^{' gpurun_out/r04a_mixed.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["output_check"]["blocks_checked_vs_golden"], d["kernels_ms"])')"
+  done
+done
 CDA_CONSENSUS=0 timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04a_probe_serial.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/r04a_probe_serial.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04a_probe.log 2>&1
