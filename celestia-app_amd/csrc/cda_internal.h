@@ -51,10 +51,6 @@ int rs_decode_init_device_tables(int device);
 int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d_stride, const uint8_t* d_present,
                      int ncw, int k, int shard_len, hipStream_t s);
 int launch_rs_encode8(const RsJob& job, hipStream_t s);
-// RS pass `job` (k = 128) and the leaf hashing of cells [g0, g0 + count) of another chunk in one launch (-2: not
-// eligible)
-int launch_rs8_mixed_leaf(const RsJob& job, const uint8_t* leaf_eds, void* leaf_nodes, unsigned long long* leaf_status,
-                          int k, uint32_t g0, uint32_t count, hipStream_t s);
 int launch_rs_encode16(const RsJob& job, hipStream_t s);
 // register-resident GF(2^16) encoder for k = 512 (rs16_kernels.hip)
 bool rs16_reg_eligible(const RsJob& j);

@@ -3,23 +3,21 @@
 // PrepareProposal and ProcessProposal extend one block per call (app/prepare_proposal.go:65-93,
 // app/process_proposal.go:137-151 -> da.ExtendShares + da.NewDataAvailabilityHeader,
 // pkg/da/data_availability_header.go:44-75), and go/cda.ExtendSharesOn hands libcda a freshly copied share buffer
-// and a NEW 4k^2 x 512 B EDS slice per call (go/cda/extend.go:42-48).  A plain pageable hipMemcpy into such a slice
-// pins it page by page in the calling thread (first-touch faults included), so the old serial form -- H2D, whole
-// pipeline, one D2H -- spent most of its time in the host side of the copies.  Here every host byte moves through
-// pinned buffers of this context with a pool of copy threads, and the copies overlap the device work:
+// and a NEW 4k^2 x 512 B EDS slice per call (go/cda/extend.go:42-48).  The serial form -- H2D, the whole pipeline,
+// one pageable D2H -- took 0.91 ms with a written output buffer but 3.6 ms with a fresh one: the runtime pins a
+// never-touched buffer page by page, faulting 8,192 pages in one thread (profiles/r04_pass1.log).  Here the copies
+// overlap the device work and the output's first touch is spread over a pool of copy threads (extend_one_host):
 //
-//   ODS    : the caller's rows are copied into a pinned slab by the pool, one row band at a time; each band's DMA is
-//            issued as soon as it is staged, and the RS row pass of that band runs as soon as its DMA lands.
+//   ODS    : up band by band, each band's RS row pass launched as soon as its copy lands.
 //   Q0     : the EDS's top-left quadrant IS the ODS (rsmt2d copies the shares in): the pool copies it host to host
 //            from the caller's ODS into the caller's EDS -- it never crosses PCIe.
 //   Q1     : each band's right halves come back (one 2-D DMA per band) right after that band's row pass.
-//   Q2|Q3  : the bottom half comes back in chunks right after the column pass, while the leaf hashing, the trees and
-//            the DAH run on the compute stream; the pool copies each chunk into the caller's slice as it lands.
-//   pages  : while the device works, the pool touches the caller's (possibly never-touched) output pages, so the
-//            first-touch faults are off the critical path and spread over the pool's threads.
-// Pinned caller buffers (cda_host_alloc / hipHostRegister) skip the staging: DMA straight to / from them.
+//   Q2|Q3  : the bottom half comes back right after the column pass, while the leaf hashing, the trees and the DAH
+//            run on the compute stream.
+//   pages  : a fresh output gets transparent huge pages and is touched by the pool while the device works.
 // k <= 256 (pinned slabs of up to 32 + 96 MiB per context); larger squares and profiling runs use the serial form.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -237,12 +235,47 @@ void touch_pages(uint8_t* p, size_t n) {
   if (n) touch_byte(p + n - 1);
 }
 
+// The caller's output pages: all resident (a buffer the caller has written before) or not (a fresh allocation,
+// first touched by this call)?  mincore over the range; a failure counts as "not resident".
+bool pages_resident(const uint8_t* p, size_t n) {
+  const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)4095, hi = ((uintptr_t)p + n + 4095) & ~(uintptr_t)4095;
+  std::vector<unsigned char> vec((hi - lo) / 4096);
+  if (mincore((void*)lo, hi - lo, vec.data()) != 0) return false;
+  size_t res = 0;
+  for (unsigned char v : vec) res += v & 1;
+  return res * 10 >= vec.size() * 9;  // >= 90 %
+}
+
+// Fresh output: ask for transparent huge pages on its 2 MiB-aligned interior before anything touches it.  The GPU box
+// runs THP in "madvise" mode; with 4 KiB pages the first-touch faults of 32 MiB did not scale past ~14 GB/s over any
+// number of threads, with huge pages 8 threads wrote fresh memory at ~58 GB/s (tools/fault_probe.cpp,
+// profiles/r04_pass1.log).  A hint on the caller's range: it changes page size, never contents.
+void want_huge_pages(uint8_t* p, size_t n) {
+  const uintptr_t lo = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+  const uintptr_t hi = ((uintptr_t)p + n) & ~(uintptr_t)((2u << 20) - 1);
+  if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_HUGEPAGE);
+}
+
 }  // namespace
 
 // The caller holds the context lock.  One block of width k (k <= 256): ods host (k^2 x 512), eds_or_null host
 // (4k^2 x 512), roots / dah / err as cda_extend_commit_batch.
+//
+// Input: the ODS goes up band by band (pageable hipMemcpyAsync: the runtime pins the caller's written pages on the
+// fly; staging them through a pinned slab with the copy pool measured slower, 0.58 vs 0.49 ms roots-only), and each
+// band's row pass runs as soon as its copy lands.  Output, by what the caller's EDS buffer is:
+//   pinned      Q1 and the bottom half straight to it by DMA;
+//   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
+//               pages cheaply and runs at the link rate;
+//   fresh       huge pages asked for, every page touched by the pool while the device works, then Q1 and the bottom
+//               half through the pinned slab in 1 MiB chunks copied out by the pool as each lands (a pageable DMA
+//               into never-touched memory faults it page by page in one thread: 3.6 ms per block, r04_pass1).
+// Q0 is always the host copy of the caller's shares.  CDA_CONS_IN=0 stages the input through the pool, 2 sends it
+// whole; CDA_CONS_OUT=1 / 2 force the fresh / resident output form (A/B runs).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  static const int in_mode = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 1;
+  static const int out_mode = getenv("CDA_CONS_OUT") ? atoi(getenv("CDA_CONS_OUT")) : 0;
   const uint32_t w = 2 * k;
   const size_t S = CDA_SHARE, rowS = (size_t)k * S, erowS = (size_t)w * S;
   const size_t ods_b = (size_t)k * rowS, eds_b = (size_t)w * erowS, q1_b = ods_b, bot_b = (size_t)k * erowS;
@@ -256,18 +289,23 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)))
     return rc;
   const bool in_pinned = pinned_host(ods);
+  const bool stage_in = !in_pinned && in_mode == 0;
   const bool want = eds_or_null != nullptr;
   const bool out_pinned = want && pinned_host(eds_or_null);
-  if ((!in_pinned && (rc = grow_pinned(c, X->pin_in, X->cap_in, ods_b))) ||
+  bool resident = false;  // output form (pinned / resident / fresh), see above
+  if (want && !out_pinned) resident = out_mode == 2 || (out_mode == 0 && pages_resident(eds_or_null, eds_b));
+  const bool fresh = want && !out_pinned && !resident;
+  if ((stage_in && (rc = grow_pinned(c, X->pin_in, X->cap_in, ods_b))) ||
       (want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + bot_b))) ||
       (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)))
     return rc;
+  if (fresh) want_huge_pages(eds_or_null, eds_b);
 
   // bands of the row pass (an even number of rows each: the FF8 encoder takes codeword pairs) and chunks of the
   // bottom half's copy-out
-  const uint32_t nband = k >= 16 ? 4 : 1, kb = k / nband;
+  const uint32_t nband = (k >= 16 && in_mode != 2) ? 4 : 1, kb = k / nband;
   const uint32_t nchunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(Consensus::kMaxChunks, bot_b >> 20));
-  const uint8_t* src_in = in_pinned ? ods : X->pin_in;
+  const uint8_t* src_in = stage_in ? X->pin_in : ods;
   uint8_t* d_ods = (uint8_t*)c->ods.p;
   uint8_t* d_eds = (uint8_t*)c->eds.p;
   uint8_t* pin_q1 = X->pin_out;
@@ -278,11 +316,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   std::atomic<int> q1_rec{0}, bot_rec{0};
   const size_t band_b = (size_t)kb * rowS;
   const int pieces_per_band = band_b >= ((size_t)1 << 20) ? 4 : 1;
-  for (uint32_t b = 0; b < nband; b++) staged[b].store(in_pinned ? 0 : pieces_per_band);
+  for (uint32_t b = 0; b < nband; b++) staged[b].store(stage_in ? pieces_per_band : 0);
 
   std::vector<std::function<void()>> tasks;
   tasks.reserve(128);
-  if (!in_pinned)  // ODS rows -> pinned slab, band by band
+  if (stage_in)  // ODS rows -> pinned slab, band by band
     for (uint32_t b = 0; b < nband; b++)
       for (int q = 0; q < pieces_per_band; q++) {
         const size_t lo = b * band_b + band_b * q / pieces_per_band, hi = b * band_b + band_b * (q + 1) / pieces_per_band;
@@ -292,7 +330,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
         });
       }
   if (want) {
-    if (!out_pinned)  // first touch of the bottom half while the device works
+    if (fresh)  // first touch of the bottom half while the device works
       for (uint32_t j = 0; j < 2 * nchunk; j++) {
         const size_t lo = bot_b * j / (2 * nchunk), hi = bot_b * (j + 1) / (2 * nchunk);
         tasks.emplace_back([=] { touch_pages(eds_or_null + k * erowS + lo, hi - lo); });
@@ -302,11 +340,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
     for (uint32_t r0 = 0; r0 < k; r0 += rows_per_task)
       tasks.emplace_back([=] {
         for (uint32_t r = r0; r < std::min(k, r0 + rows_per_task); r++) {
-          if (!out_pinned) touch_pages(eds_or_null + r * erowS + rowS, rowS);
+          if (fresh) touch_pages(eds_or_null + r * erowS + rowS, rowS);
           memcpy(eds_or_null + r * erowS, ods + r * rowS, rowS);
         }
       });
-    if (!out_pinned) {
+    if (!out_pinned)
       for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its 2-D DMA has landed
         for (uint32_t r0 = b * kb; r0 < (b + 1) * kb; r0 += rows_per_task)
           tasks.emplace_back([=, &q1_rec, &abort] {
@@ -314,6 +352,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
             for (uint32_t r = r0; r < std::min((b + 1) * kb, r0 + rows_per_task); r++)
               memcpy(eds_or_null + r * erowS + rowS, pin_q1 + r * rowS, rowS);
           });
+    if (fresh)
       for (uint32_t j = 0; j < nchunk; j++) {  // bottom-half chunk j (1 MiB at k = 128), four tasks each: the last
                                                // chunk's host copy is on the critical path
         const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
@@ -325,11 +364,10 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
           });
         }
       }
-    }
   }
   X->pool->start(&tasks);
 
-  // device work, issued band by band as the staging lands
+  // device work, issued band by band as the input lands
   hipStream_t s = c->stream;
   const char* fail = nullptr;
   int frc = CDA_OK;
@@ -376,7 +414,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   if (!fail && want) {
     if (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess)
       fail = "event";
-    for (uint32_t j = 0; j < nchunk && !fail; j++) {
+    for (uint32_t j = 0; j < nchunk && !fail && !resident; j++) {
       const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
       uint8_t* dst = out_pinned ? eds_or_null + k * erowS + lo : pin_bot + lo;
       if (hipMemcpyAsync(dst, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
@@ -398,6 +436,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       fail = "results D2H";
     }
   }
+  // resident output: the bottom half by one pageable DMA (this thread waits in it while the pool copies Q0 / Q1)
+  if (!fail && resident &&
+      hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
+          hipSuccess)
+    fail = "bottom D2H";
   if (fail) abort.store(true);
   X->pool->help_and_wait();
   if (!fail) wait_event(X->ev_done, abort);

@@ -260,38 +260,6 @@ int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ed
   return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, rec_off);
 }
 
-// CDA_MIXED=C (experiment): the batch in C chunks; the RS rows / columns of chunk i+1 each share a
-// launch with half of chunk i's leaf hashing (rs8_mixed_leaf_kernel), then chunk C-1's leaves, then every tree.
-static int enqueue_pipeline_mixed(cda_ctx* c, uint32_t k, uint32_t nblocks, uint32_t C, const uint8_t* d_ods,
-                                  uint8_t* d_eds, void* d_roots, void* d_dah, unsigned long long* d_status,
-                                  hipStream_t s) {
-  const uint32_t w = 2 * k, cb = nblocks / C, cells = cb * w * w;
-  const size_t ods_blk = (size_t)k * k * CDA_SHARE, eds_blk = (size_t)w * w * CDA_SHARE;
-  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
-  auto leaf_at = [&](uint32_t i) { return (uint8_t*)c->leaf.p + (size_t)i * cells * CDA_REC_BYTES; };
-  for (uint32_t i = 0; i < C; i++) {
-    const RsJob rj = rows_job(k, cb, d_ods + i * cb * ods_blk, d_eds + i * cb * eds_blk);
-    const RsJob cj = cols_job(k, cb, d_eds + i * cb * eds_blk);
-    if (i == 0) {
-      ProfScope ps(c, "mixed_rs0", s);
-      if (launch_rs_encode8(rj, s) || launch_rs_encode8(cj, s)) return CDA_E_DEVICE;
-      continue;
-    }
-    const uint8_t* pe = d_eds + (i - 1) * cb * eds_blk;
-    unsigned long long* pst = d_status + (i - 1) * cb;
-    ProfScope ps(c, "mixed_rs_leaf", s);
-    if (launch_rs8_mixed_leaf(rj, pe, leaf_at(i - 1), pst, (int)k, 0, cells / 2, s) ||
-        launch_rs8_mixed_leaf(cj, pe, leaf_at(i - 1), pst, (int)k, cells / 2, cells - cells / 2, s))
-      return CDA_E_DEVICE;
-  }
-  {
-    ProfScope ps(c, "leaf_hash", s);
-    if (launch_leaf_hash(d_eds + (C - 1) * cb * eds_blk, leaf_at(C - 1), d_status + (C - 1) * cb, (int)k, (int)cb, s))
-      return CDA_E_DEVICE;
-  }
-  return enqueue_trees(c, k, nblocks, d_roots, d_dah, s, 0);
-}
-
 int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, void* d_roots,
                      void* d_dah, unsigned long long* d_status, hipStream_t s) {
   // One stream, one kernel per stage: each stage already fills the GPU.  Measured slower and removed
@@ -303,9 +271,6 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (rc) return rc;
   rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES);  // inner tree levels
   if (rc) return rc;
-  static const uint32_t mixed = getenv("CDA_MIXED") ? (uint32_t)atoi(getenv("CDA_MIXED")) : 0u;
-  if (mixed > 1 && k == 128 && nblocks % mixed == 0)
-    return enqueue_pipeline_mixed(c, k, nblocks, mixed, d_ods, d_eds, d_roots, d_dah, d_status, s);
   if ((rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s))) return rc;
   return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, 0);
 }

@@ -233,9 +233,7 @@ __device__ __forceinline__ void rfc_node_block(const uint32_t* Ld, const uint32_
 // a level has at most 64 nodes (its chain of dependent compressions is the latency), wave 0 hashes block 0 of each
 // node while wave 1 expands the node's second message block into kw (64 x kKwStride words of LDS), and the second
 // compression then runs its rounds alone.
-__device__ __forceinline__ void dah_fold_kw(uint32_t* sdig, int n, uint32_t* out, uint32_t* kw,
-                                            uint32_t* kw0 = nullptr) {
-  // kw0 (64 more rows): block 0 too runs its rounds 16..63 from a helper-expanded schedule (sha256_rounds16)
+__device__ __forceinline__ void dah_fold_kw(uint32_t* sdig, int n, uint32_t* out, uint32_t* kw) {
   uint32_t* src = sdig;
   uint32_t* dst = sdig + n * 8;
   for (int cnt = n; cnt > 1;) {
@@ -262,45 +260,25 @@ __device__ __forceinline__ void dah_fold_kw(uint32_t* sdig, int n, uint32_t* out
     } else {
       const int i = threadIdx.x & 63;
       const bool pair = i < out_cnt && 2 * i + 1 < cnt;
-      const bool work = threadIdx.x < 64, help = threadIdx.x >= 64 && threadIdx.x < 128;
-      uint32_t st[8], v[8];
-      if (work && i < out_cnt) {
+      uint32_t st[8];
+      if (threadIdx.x < 64 && i < out_cnt) {
         const uint32_t* Ld = src + (2 * i) * 8;
         if (pair) {
           uint32_t m[16];
           sha256_init(st);
           rfc_node_block<0>(Ld, src + (2 * i + 1) * 8, m);
-          if (kw0) {
-#pragma unroll
-            for (int t = 0; t < 8; t++) v[t] = st[t];
-            sha256_rounds16(v, m);
-          } else {
-            sha256_compress(st, m);
-          }
+          sha256_compress(st, m);
         } else {
 #pragma unroll
           for (int t = 0; t < 8; t++) dst[i * 8 + t] = Ld[t];
         }
-      } else if (help && pair && kw0) {
-        uint32_t m[16];
-        rfc_node_block<0>(src + (2 * i) * 8, src + (2 * i + 1) * 8, m);
-        sha256_kw48_store(m, kw0 + i * kKwStride);
-      }
-      if (kw0) {
-        __syncthreads();
-        if (work && pair) {
-          sha256_rounds_kw48(v, kw0 + i * kKwStride);
-#pragma unroll
-          for (int t = 0; t < 8; t++) st[t] += v[t];
-        }
-      }
-      if (help && pair) {
+      } else if (threadIdx.x >= 64 && threadIdx.x < 128 && pair) {
         uint32_t m[16];
         rfc_node_block<1>(src + (2 * i) * 8, src + (2 * i + 1) * 8, m);
         sha256_kw_store(m, kw + i * kKwStride);
       }
       __syncthreads();
-      if (work && pair) {
+      if (threadIdx.x < 64 && pair) {
         sha256_rounds_kw(st, kw + i * kKwStride);
 #pragma unroll
         for (int t = 0; t < 8; t++) dst[i * 8 + t] = st[t];
@@ -420,34 +398,16 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
         for (int q = 0; q < 6; q++) out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
       }
     } else {
-      // wave 0 of the half runs rounds 0..15 of block 0 of node ht from the message words while wave 1 expands
-      // block 0's W16..63; after a barrier wave 0 runs rounds 16..63 while wave 1 expands blocks 1 and 2; after a
-      // second barrier wave 0 runs the last two compressions from the precomputed schedules.  On the dependent chain
-      // per level: about 3 x 900 instructions instead of 1,440 + 2 x 900.
+      // wave 0 of the half hashes block 0 of node ht while wave 1 expands blocks 1 and 2 of node ht - 64; after
+      // the barrier wave 0 runs the last two compressions from the precomputed schedules
       const int i = ht & 63;
-      uint32_t L[24], R[24], st[8], v[8];
+      uint32_t L[24], R[24], st[8];
       if (i < nodes) load_pair(in, i, L, R);
-      // block 0's schedule rows: at w = 256 in A's records 64.. (from level 2 on a level reads or writes only
-      // A[0..64)); for smaller trees in rows of their own after the block 1 / 2 rows
-      // (rows: [half 0 blocks 1, 2 | half 1 blocks 1, 2 | half 0 block 0 | half 1 block 0], kw = this half's first)
-      uint32_t* kw0 = w == 256 ? reinterpret_cast<uint32_t*>(A + 64 * kLdsRec) : kw + (4 - half) * 64 * kKwStride;
       if (ht < 64 && i < nodes) {
         uint32_t m[16];
         sha256_init(st);
         node_block<0>(L, R, m);
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = st[j];
-        sha256_rounds16(v, m);
-      } else if (ht >= 64 && i < nodes) {
-        uint32_t m[16];
-        node_block<0>(L, R, m);
-        sha256_kw48_store(m, kw0 + i * kKwStride);
-      }
-      __syncthreads();
-      if (ht < 64 && i < nodes) {
-        sha256_rounds_kw48(v, kw0 + i * kKwStride);
-#pragma unroll
-        for (int j = 0; j < 8; j++) st[j] += v[j];
+        sha256_compress(st, m);
       } else if (ht >= 64 && i < nodes) {
         uint32_t m[16];
         node_block<1>(L, R, m);
@@ -470,9 +430,8 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   const uint4* root = (log2w & 1) ? B : A;
   uint4* rout = roots + ((size_t)b * n + tree) * 6;
   if (ht < 6) rout[ht] = root[ht];
-  {  // this root's DAH leaf digest: rounds 0..15 of block 0 by lane 0 while lane 64 expands block 0's schedule, then
-     // rounds 16..63 while lane 64 expands block 1's, then block 1's rounds
-    uint32_t L[24], st[8], v[8], m[16];
+  {  // this root's DAH leaf digest: block 0 by lane 0, block 1's schedule by lane 64 meanwhile
+    uint32_t L[24], st[8], m[16];
     if (ht == 0 || ht == 64) {
 #pragma unroll
       for (int q = 0; q < 6; q++) {
@@ -480,22 +439,10 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
         L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
       }
     }
-    uint32_t* kw0 = kw + 64 * kKwStride;  // this half's block-2 rows, idle once the levels are done
     if (ht == 0) {
       sha256_init(st);
       dah_leaf_block<0>(L, m);
-#pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = st[j];
-      sha256_rounds16(v, m);
-    } else if (ht == 64) {
-      dah_leaf_block<0>(L, m);
-      sha256_kw48_store(m, kw0);
-    }
-    __syncthreads();
-    if (ht == 0) {
-      sha256_rounds_kw48(v, kw0);
-#pragma unroll
-      for (int j = 0; j < 8; j++) st[j] += v[j];
+      sha256_compress(st, m);
     } else if (ht == 64) {
       dah_leaf_block<1>(L, m);
       sha256_kw_store(m, kw);
@@ -520,8 +467,7 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   const uint4* src = reinterpret_cast<const uint4*>(digests + (size_t)b * n * 8);
   for (int x = threadIdx.x; x < n * 2; x += blockDim.x) reinterpret_cast<uint4*>(sdig)[x] = src[x];
   __syncthreads();
-  uint32_t* fkw = sdig + (n + (n + 1) / 2) * 8;  // 64 rows for block 1, then 64 for block 0
-  dah_fold_kw(sdig, n, dah + b * 8, fkw, fkw + 64 * kKwStride);
+  dah_fold_kw(sdig, n, dah + b * 8, sdig + (n + (n + 1) / 2) * 8);
   if (threadIdx.x == 0) __hip_atomic_store(done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -636,12 +582,10 @@ int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned*
   while ((1 << log2w) < w) log2w++;
   if ((1 << log2w) != w || log2w < 1) return -2;
   if (w > 256) return -2;  // a thread per node of level 1 within a 128-thread half
-  // two trees x (w + w / 2) records of 112 B, then 2 x 2 x 64 schedule rows of kKwStride words (blocks 1, 2), and for
-  // w < 256 2 x 64 more (block 0; at w = 256 those sit in the idle part of A); the DAH fold reuses it: (2w + w) x 32 B
-  // of digests + 2 x 64 schedule rows
-  const size_t lds = 2 * ((size_t)w + w / 2 + 1) * kLdsRec * 16 + (size_t)(w == 256 ? 4 : 6) * 64 * kKwStride * 4;
-  if ((size_t)(2 * w + w) * 32 + (size_t)2 * 64 * kKwStride * 4 > lds) return -2;
-  static_assert(64 * kKwStride * 4 <= (256 - 64) * kLdsRec * 16, "block-0 schedule rows fit A's idle records");
+  // two trees x (w + w / 2) records of 112 B, then 2 x 2 x 64 schedule rows of kKwStride words; the DAH fold
+  // reuses it: (2w + w) x 32 B of digests + 64 schedule rows
+  const size_t lds = 2 * ((size_t)w + w / 2 + 1) * kLdsRec * 16 + (size_t)4 * 64 * kKwStride * 4;
+  if ((size_t)(2 * w + w) * 32 + (size_t)64 * kKwStride * 4 > lds) return -2;
   // the dynamic-LDS limit is raised to what the launch needs: 160 KiB would exceed the CU's LDS by the kernel's
   // static __shared__ word and the call would fail (and with it the launch)
   if (lds > 64 * 1024 &&

@@ -30,7 +30,6 @@
 #include "cda_internal.h"
 #include "gf8_const.h"
 #include "gf_slice.h"
-#include "nmt_dev.h"
 
 namespace cda {
 
@@ -521,47 +520,7 @@ __global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegA
   rs_g2_body<L>(a, wg, xbuf);
 }
 
-// ---- one launch, two roles (a bounded experiment): the RS pass of one chunk of blocks beside the
-// leaf hashing of the previous chunk.  The RS waves wait on HBM about half of their time while the SHA-256 waves
-// are VALU-bound; separate streams never put them on one CU together (each kernel fills the GPU and the next one's
-// workgroups only start as the first one's retire), a single launch does by construction: workgroup b is an RS
-// workgroup or a leaf workgroup by an even (Bresenham) interleave of the two counts.  k = 128 only (L = 7).
-struct LeafPart {
-  const uint8_t* eds;
-  uint4* nodes;
-  unsigned long long* status;
-  int k, log2w;
-  uint32_t g0, count;  // cells [g0, g0 + count) of the chunk (gid as leaf_hash_kernel's)
-};
-__global__ void __launch_bounds__(512, 4) rs8_mixed_leaf_kernel(Rs8RegArgs a, LeafPart lp, unsigned nrs,
-                                                                unsigned nleaf) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xbuf[];
-  const unsigned b = blockIdx.x, tot = nrs + nleaf;
-  const unsigned r0 = (unsigned)(((unsigned long long)b * nrs) / tot);
-  const unsigned r1 = (unsigned)(((unsigned long long)(b + 1) * nrs) / tot);
-  if (r1 > r0) {  // RS workgroup number r0
-    rs_g2_body<7>(a, (int)r0, xbuf);
-    return;
-  }
-  const uint32_t gid = lp.g0 + (b - r0) * 512u + threadIdx.x;  // b - r0 leaf workgroups precede this one
-  if (gid < lp.g0 + lp.count) leaf_cell(lp.eds, lp.nodes, lp.status, lp.k, lp.log2w, gid);
-}
-
 static Rs8RegArgs reg_args(const RsJob& j);
-
-int launch_rs8_mixed_leaf(const RsJob& j, const uint8_t* leaf_eds, void* leaf_nodes, unsigned long long* leaf_status,
-                          int k, uint32_t g0, uint32_t count, hipStream_t s) {
-  if (j.k != 128 || j.cw_per_blk % 2 || j.shard_len % 512 || k != 128) return -2;
-  Rs8RegArgs r = reg_args(j);
-  r.remap = 0;
-  const long long nrs = (long long)j.nblk * r.groups_per_blk * r.slices;
-  const long long nleaf = ((long long)count + 511) / 512;
-  if (nrs <= 0 || nrs + nleaf > 0x7FFFFFFF) return -2;
-  LeafPart lp{leaf_eds, (uint4*)leaf_nodes, leaf_status, k, 8, g0, count};
-  hipLaunchKernelGGL(rs8_mixed_leaf_kernel, dim3((unsigned)(nrs + nleaf)), dim3(512), (size_t)128 * 32 * 16, s, r, lp,
-                     (unsigned)nrs, (unsigned)nleaf);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 int rs_init_device_tables(int device) {
   (void)device;
@@ -592,9 +551,6 @@ int rs_init_device_tables(int device) {
                         (const void*)rs_encode8_g2_kernel<6>, (const void*)rs_encode8_g2_kernel<7>};
   for (auto f : g2k)
     if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) != hipSuccess) return -1;
-  if (hipFuncSetAttribute((const void*)rs8_mixed_leaf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) !=
-      hipSuccess)
-    return -1;
 
   return 0;
 }

@@ -159,60 +159,6 @@ __device__ __forceinline__ void sha256_rounds_kw(uint32_t s[8], const uint32_t* 
   s[7] += h;
 }
 
-// Block 0 of a node depends on its children, so its schedule cannot be expanded before the chain reaches it; but
-// rounds 0..15 need only the message words themselves.  The working wave runs those (sha256_rounds16) while a helper
-// wave expands W16..63 (sha256_kw48_store: 12 x 16 B of K + W), and after one barrier the working wave runs rounds
-// 16..63 from them (sha256_rounds_kw48): a dependent block-0 compression costs ~14 x 64 instructions instead of
-// ~1,440.  v[8] = the working variables a..h (the chaining state is added back by the caller).
-__device__ __forceinline__ void sha256_round(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
-                                             uint32_t& f, uint32_t& g, uint32_t& h, uint32_t kw) {
-  const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + kw;
-  const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
-  h = g;
-  g = f;
-  f = e;
-  e = d + t1;
-  d = c;
-  c = b;
-  b = a;
-  a = t1 + t2;
-}
-__device__ __forceinline__ void sha256_rounds16(uint32_t (&v)[8], const uint32_t (&w)[16]) {
-  uint32_t a = v[0], b = v[1], c = v[2], d = v[3], e = v[4], f = v[5], g = v[6], h = v[7];
-#pragma unroll
-  for (int t = 0; t < 16; t++) sha256_round(a, b, c, d, e, f, g, h, K256::v[t] + w[t]);
-  v[0] = a, v[1] = b, v[2] = c, v[3] = d, v[4] = e, v[5] = f, v[6] = g, v[7] = h;
-}
-__device__ __forceinline__ void sha256_kw48_store(uint32_t (&w)[16], uint32_t* kw) {
-#pragma unroll
-  for (int t4 = 4; t4 < 16; t4++) {
-    uint32_t x[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int t = 4 * t4 + j;
-      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-      const uint32_t wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-      w[t & 15] = wt;
-      x[j] = wt + K256::v[t];
-    }
-    reinterpret_cast<uint4*>(kw)[t4 - 4] = make_uint4(x[0], x[1], x[2], x[3]);
-  }
-}
-__device__ __forceinline__ void sha256_rounds_kw48(uint32_t (&v)[8], const uint32_t* kw) {
-  uint32_t a = v[0], b = v[1], c = v[2], d = v[3], e = v[4], f = v[5], g = v[6], h = v[7];
-#pragma unroll
-  for (int t4 = 0; t4 < 12; t4++) {
-    const uint4 q = reinterpret_cast<const uint4*>(kw)[t4];
-    sha256_round(a, b, c, d, e, f, g, h, q.x);
-    sha256_round(a, b, c, d, e, f, g, h, q.y);
-    sha256_round(a, b, c, d, e, f, g, h, q.z);
-    sha256_round(a, b, c, d, e, f, g, h, q.w);
-  }
-  v[0] = a, v[1] = b, v[2] = c, v[3] = d, v[4] = e, v[5] = f, v[6] = g, v[7] = h;
-}
-
 // N independent compressions advanced in lockstep (round-interleaved), giving
 // the scheduler N independent dependency chains per wave.
 template <int N, int SB = 0>

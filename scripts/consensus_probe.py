@@ -48,13 +48,13 @@ def series(want_eds, fresh_out):
     return {"min": round(min(out), 3), "median": round(float(np.median(out)), 3), "max": round(max(out), 3)}
 
 
-res = {"reps": reps, "consensus": os.environ.get("CDA_CONSENSUS", "1")}
+res = {"reps": reps, **{v: os.environ[v] for v in ("CDA_CONSENSUS", "CDA_CONS_IN", "CDA_CONS_OUT") if v in os.environ}}
 res["fresh_with_eds"] = series(True, True)
 res["fresh_roots_only"] = series(False, True)
 res["reused_with_eds"] = series(True, False)
 res["reused_roots_only"] = series(False, False)
 print(json.dumps(res), flush=True)
-if os.environ.get("CDA_CONSENSUS", "1") != "0":  # copy-pool size sweep (a context reads CDA_COPY_THREADS at its first call)
+if os.environ.get("CDA_CONSENSUS", "1") != "0" and os.environ.get("CDA_PROBE_SWEEP"):  # copy-pool size sweep (a context reads CDA_COPY_THREADS at its first call)
     sweep = {}
     for T in (3, 7, 11, 15):
         os.environ["CDA_COPY_THREADS"] = str(T)
@@ -64,6 +64,8 @@ if os.environ.get("CDA_CONSENSUS", "1") != "0":  # copy-pool size sweep (a conte
     os.environ.pop("CDA_COPY_THREADS")
     print(json.dumps({"copy_threads_sweep_fresh_with_eds": sweep}), flush=True)
 
+if not os.environ.get("CDA_PROBE_HOST"):
+    sys.exit(0)
 # host side: first-touch copies into fresh pages
 N = 32 << 20
 src = torch.empty(N, dtype=torch.uint8).pin_memory().numpy()
