@@ -261,20 +261,20 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // The caller holds the context lock.  One block of width k (k <= 256): ods host (k^2 x 512), eds_or_null host
 // (4k^2 x 512), roots / dah / err as cda_extend_commit_batch.
 //
-// Input: the ODS goes up band by band (pageable hipMemcpyAsync: the runtime pins the caller's written pages on the
-// fly; staging them through a pinned slab with the copy pool measured slower, 0.58 vs 0.49 ms roots-only), and each
-// band's row pass runs as soon as its copy lands.  Output, by what the caller's EDS buffer is:
+// Input: the ODS goes up in one pageable hipMemcpyAsync (the runtime pins the caller's written pages on the fly):
+// roots-only 0.467 ms per block, against 0.553 ms in four bands (each pageable copy pays its own setup) and 0.59 ms
+// staged through a pinned slab by the copy pool (profiles/r04_pass2.log).  Output, by what the caller's EDS buffer is:
 //   pinned      Q1 and the bottom half straight to it by DMA;
 //   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
 //               pages cheaply and runs at the link rate;
 //   fresh       huge pages asked for, every page touched by the pool while the device works, then Q1 and the bottom
 //               half through the pinned slab in 1 MiB chunks copied out by the pool as each lands (a pageable DMA
 //               into never-touched memory faults it page by page in one thread: 3.6 ms per block, r04_pass1).
-// Q0 is always the host copy of the caller's shares.  CDA_CONS_IN=0 stages the input through the pool, 2 sends it
-// whole; CDA_CONS_OUT=1 / 2 force the fresh / resident output form (A/B runs).
+// Q0 is always the host copy of the caller's shares.  CDA_CONS_IN=0 stages the input through the pool, 1 sends it in
+// four bands; CDA_CONS_OUT=1 / 2 force the fresh / resident output form (A/B runs).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
-  static const int in_mode = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 1;
+  static const int in_mode = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 2;
   static const int out_mode = getenv("CDA_CONS_OUT") ? atoi(getenv("CDA_CONS_OUT")) : 0;
   const uint32_t w = 2 * k;
   const size_t S = CDA_SHARE, rowS = (size_t)k * S, erowS = (size_t)w * S;
