@@ -20,6 +20,8 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -130,7 +132,7 @@ struct Consensus {
   uint8_t* pin_res = nullptr;  // 4k root records | DAH | status
   size_t cap_in = 0, cap_out = 0, cap_res = 0;
   hipEvent_t ev_in[kMaxBands] = {}, ev_rows[kMaxBands] = {}, ev_q1[kMaxBands] = {}, ev_cols = nullptr,
-             ev_bot[kMaxChunks] = {}, ev_done = nullptr;
+             ev_bot[kMaxChunks] = {}, ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr;
   ~Consensus() {
     delete pool;
     for (uint8_t* p : {pin_in, pin_out, pin_res})
@@ -140,7 +142,7 @@ struct Consensus {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_bot)
       if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_cols, ev_done})
+    for (hipEvent_t e : {ev_cols, ev_done, ev_h2d_end, ev_d2h_end})
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -185,7 +187,9 @@ int get_consensus(cda_ctx* c, Consensus*& out) {
     for (int i = 0; i < Consensus::kMaxChunks && ok; i++)
       ok = hipEventCreateWithFlags(&s->ev_bot[i], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&s->ev_cols, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&s->ev_h2d_end, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&s->ev_d2h_end, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
       delete s;
       c->last_err = "consensus path: event creation failed";
@@ -235,15 +239,21 @@ void touch_pages(uint8_t* p, size_t n) {
   if (n) touch_byte(p + n - 1);
 }
 
-// The caller's output pages: all resident (a buffer the caller has written before) or not (a fresh allocation,
-// first touched by this call)?  mincore over the range; a failure counts as "not resident".
+// The caller's output pages: resident (a buffer the caller has written before) or not (a fresh allocation, first
+// touched by this call)?  mincore over four 64 KiB windows spread over the range (a whole-range mincore walks 8 K
+// page-table entries per call); a failure counts as "not resident".  Either answer is correct for any buffer -- a
+// partly resident one only takes the slower form.
 bool pages_resident(const uint8_t* p, size_t n) {
-  const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)4095, hi = ((uintptr_t)p + n + 4095) & ~(uintptr_t)4095;
-  std::vector<unsigned char> vec((hi - lo) / 4096);
-  if (mincore((void*)lo, hi - lo, vec.data()) != 0) return false;
-  size_t res = 0;
-  for (unsigned char v : vec) res += v & 1;
-  return res * 10 >= vec.size() * 9;  // >= 90 %
+  unsigned char vec[16];
+  for (int i = 0; i < 4; i++) {
+    const uintptr_t at = ((uintptr_t)p + (n - std::min<size_t>(n, 65536)) * i / 3) & ~(uintptr_t)4095;
+    const size_t len = std::min<size_t>(65536, (uintptr_t)p + n - at) & ~(size_t)4095;
+    if (!len) continue;
+    if (mincore((void*)at, len, vec) != 0) return false;
+    for (size_t j = 0; j < len / 4096; j++)
+      if (!(vec[j] & 1)) return false;
+  }
+  return true;
 }
 
 // Fresh output: ask for transparent huge pages on its 2 MiB-aligned interior before anything touches it.  The GPU box
@@ -267,15 +277,25 @@ void want_huge_pages(uint8_t* p, size_t n) {
 //   pinned      Q1 and the bottom half straight to it by DMA;
 //   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
 //               pages cheaply and runs at the link rate;
-//   fresh       huge pages asked for, every page touched by the pool while the device works, then Q1 and the bottom
-//               half through the pinned slab in 1 MiB chunks copied out by the pool as each lands (a pageable DMA
-//               into never-touched memory faults it page by page in one thread: 3.6 ms per block, r04_pass1).
+//   fresh       huge pages asked for and every page first touched by the pool (one 2 MiB page per task, the tasks
+//               of distinct pages first) while the device works, then the resident form: a pageable DMA into
+//               never-touched memory faults it page by page in one thread (3.6 ms per block, r04_pass1), and the
+//               earlier fresh form that sent the bottom half through the pinned slab in 1 MiB chunks copied out by
+//               the pool took 1.02-1.23 ms against 0.80-0.88 ms for this one (r04_pass4.log).
 // Q0 is always the host copy of the caller's shares.  CDA_CONS_IN=0 stages the input through the pool, 1 sends it in
-// four bands; CDA_CONS_OUT=1 / 2 force the fresh / resident output form (A/B runs).
+// four bands; CDA_CONS_OUT=1 takes the staged fresh form, 2 forces the resident form on any buffer (A/B
+// runs).  Registering the bottom half (hipHostRegister, plain async DMA, unregistered before returning) measured no
+// faster than the pageable DMA (r04_pass4.log).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
   static const int in_mode = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 2;
   static const int out_mode = getenv("CDA_CONS_OUT") ? atoi(getenv("CDA_CONS_OUT")) : 0;
+  static const bool trace = getenv("CDA_CONS_TRACE") != nullptr;  // host-side phase timestamps on stderr (A/B runs)
+  double tr[10] = {0};
+  const auto t_start = std::chrono::steady_clock::now();
+  auto mark = [&](int i) {
+    if (trace) tr[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_start).count();
+  };
   const uint32_t w = 2 * k;
   const size_t S = CDA_SHARE, rowS = (size_t)k * S, erowS = (size_t)w * S;
   const size_t ods_b = (size_t)k * rowS, eds_b = (size_t)w * erowS, q1_b = ods_b, bot_b = (size_t)k * erowS;
@@ -293,8 +313,9 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const bool want = eds_or_null != nullptr;
   const bool out_pinned = want && pinned_host(eds_or_null);
   bool resident = false;  // output form (pinned / resident / fresh), see above
-  if (want && !out_pinned) resident = out_mode == 2 || (out_mode == 0 && pages_resident(eds_or_null, eds_b));
+  if (want && !out_pinned) resident = out_mode == 2 || (out_mode != 1 && pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
+  const bool fresh_direct = fresh && out_mode != 1;  // touched by the pool, then the resident form
   if ((stage_in && (rc = grow_pinned(c, X->pin_in, X->cap_in, ods_b))) ||
       (want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + bot_b))) ||
       (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)))
@@ -314,6 +335,12 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   std::atomic<bool> abort{false};
   std::atomic<int> staged[Consensus::kMaxBands];
   std::atomic<int> q1_rec{0}, bot_rec{0};
+  // fresh output: the bottom half goes down in n_piece pieces (two huge pages each), each DMA'd once the pool has
+  // touched its pages, so the DMA of the first pieces overlaps the faults of the later ones
+  std::atomic<int> touched[Consensus::kMaxChunks];
+  const int n_touch = fresh ? (int)std::max<size_t>(1, bot_b >> 21) : 0;
+  const int n_piece = fresh_direct ? std::min(Consensus::kMaxChunks, std::max(1, n_touch / 2)) : 1;
+  for (int p = 0; p < Consensus::kMaxChunks; p++) touched[p].store(0);
   const size_t band_b = (size_t)kb * rowS;
   const int pieces_per_band = band_b >= ((size_t)1 << 20) ? 4 : 1;
   for (uint32_t b = 0; b < nband; b++) staged[b].store(stage_in ? pieces_per_band : 0);
@@ -330,20 +357,29 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
         });
       }
   if (want) {
-    if (fresh)  // first touch of the bottom half while the device works
-      for (uint32_t j = 0; j < 2 * nchunk; j++) {
-        const size_t lo = bot_b * j / (2 * nchunk), hi = bot_b * (j + 1) / (2 * nchunk);
-        tasks.emplace_back([=] { touch_pages(eds_or_null + k * erowS + lo, hi - lo); });
+    if (fresh)  // first touch of the bottom half while the device works: one 2 MiB range (a huge page) per task
+      for (int j = 0; j < n_touch; j++) {
+        const size_t lo = bot_b * j / n_touch, hi = bot_b * (j + 1) / n_touch;
+        const int piece = j * n_piece / n_touch;
+        tasks.emplace_back([=, &touched] {
+          touch_pages(eds_or_null + k * erowS + lo, hi - lo);
+          touched[piece].fetch_add(1, std::memory_order_acq_rel);
+        });
       }
-    // Q0 = the shares, host to host (and the first touch of each row's Q1 half)
+    // Q0 = the shares, host to host (and the first touch of each row's Q1 half); a task covers 1 MiB of EDS rows at
+    // k = 128, and the even tasks go first so that the first faults land on distinct huge pages
     const uint32_t rows_per_task = std::max<uint32_t>(1, (uint32_t)(((size_t)512 << 10) / rowS));
-    for (uint32_t r0 = 0; r0 < k; r0 += rows_per_task)
-      tasks.emplace_back([=] {
-        for (uint32_t r = r0; r < std::min(k, r0 + rows_per_task); r++) {
-          if (fresh) touch_pages(eds_or_null + r * erowS + rowS, rowS);
-          memcpy(eds_or_null + r * erowS, ods + r * rowS, rowS);
-        }
-      });
+    const uint32_t n_q0 = (k + rows_per_task - 1) / rows_per_task;
+    for (uint32_t half = 0; half < 2; half++)
+      for (uint32_t t = half; t < n_q0; t += 2) {
+        const uint32_t r0 = t * rows_per_task;
+        tasks.emplace_back([=] {
+          for (uint32_t r = r0; r < std::min(k, r0 + rows_per_task); r++) {
+            if (fresh) touch_pages(eds_or_null + r * erowS + rowS, rowS);
+            memcpy(eds_or_null + r * erowS, ods + r * rowS, rowS);
+          }
+        });
+      }
     if (!out_pinned)
       for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its 2-D DMA has landed
         for (uint32_t r0 = b * kb; r0 < (b + 1) * kb; r0 += rows_per_task)
@@ -352,7 +388,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
             for (uint32_t r = r0; r < std::min((b + 1) * kb, r0 + rows_per_task); r++)
               memcpy(eds_or_null + r * erowS + rowS, pin_q1 + r * rowS, rowS);
           });
-    if (fresh)
+    if (fresh && !fresh_direct)
       for (uint32_t j = 0; j < nchunk; j++) {  // bottom-half chunk j (1 MiB at k = 128), four tasks each: the last
                                                // chunk's host copy is on the critical path
         const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
@@ -366,6 +402,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       }
   }
   X->pool->start(&tasks);
+  mark(1);
 
   // device work, issued band by band as the input lands
   hipStream_t s = c->stream;
@@ -404,6 +441,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       q1_rec.store((int)b + 1, std::memory_order_release);
     }
   }
+  mark(2);
   if (!fail) {
     const RsJob j = cols_job(k, 1, d_eds);
     if (const int lr = 2 * k <= 256 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s)) {
@@ -414,7 +452,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   if (!fail && want) {
     if (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess)
       fail = "event";
-    for (uint32_t j = 0; j < nchunk && !fail && !resident; j++) {
+    for (uint32_t j = 0; j < nchunk && !fail && !resident && !fresh_direct; j++) {
       const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
       uint8_t* dst = out_pinned ? eds_or_null + k * erowS + lo : pin_bot + lo;
       if (hipMemcpyAsync(dst, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
@@ -436,17 +474,45 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       fail = "results D2H";
     }
   }
-  // resident output: the bottom half by one pageable DMA (this thread waits in it while the pool copies Q0 / Q1)
-  if (!fail && resident &&
-      hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
-          hipSuccess)
-    fail = "bottom D2H";
+  mark(3);
+  // resident output: the bottom half by one pageable DMA (this thread waits in it while the pool copies Q0 / Q1);
+  // fresh_direct: the same once the pool has touched every page of it
+  mark(4);
+  for (int p = 0; p < n_piece && !fail && (resident || fresh_direct); p++) {
+    if (fresh_direct) {  // the touch tasks of piece p: j with j * n_piece / n_touch == p
+      const int need = (int)(((int64_t)(p + 1) * n_touch + n_piece - 1) / n_piece - ((int64_t)p * n_touch + n_piece - 1) / n_piece);
+      while (touched[p].load(std::memory_order_acquire) < need) {
+        if (abort.load(std::memory_order_relaxed)) break;
+        std::this_thread::yield();
+      }
+    }
+    const size_t lo = bot_b * p / n_piece, hi = bot_b * (p + 1) / n_piece;
+    if (hipMemcpyAsync(eds_or_null + k * erowS + lo, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost,
+                       c->d2h_stream) != hipSuccess)
+      fail = "bottom D2H";
+  }
+  if (!fail && (hipEventRecord(X->ev_h2d_end, c->h2d_stream) != hipSuccess ||
+                hipEventRecord(X->ev_d2h_end, c->d2h_stream) != hipSuccess))
+    fail = "event";
+  mark(5);
   if (fail) abort.store(true);
   X->pool->help_and_wait();
+  mark(6);
   if (!fail) wait_event(X->ev_done, abort);
-  // every DMA of this call has finished before the caller's buffers (or the staging) can be touched again
-  const bool synced = hipStreamSynchronize(c->h2d_stream) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
-                      hipStreamSynchronize(c->d2h_stream) == hipSuccess;
+  mark(7);
+  // every DMA of this call has finished before the caller's buffers (or the staging) can be touched again: the
+  // streams' end events (a stream sync costs ~6 us per stream here), or whole-stream syncs after a failure
+  bool synced;
+  if (!fail && !abort.load())
+    synced = wait_event(X->ev_h2d_end, abort) && wait_event(X->ev_d2h_end, abort);
+  else
+    synced = hipStreamSynchronize(c->h2d_stream) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
+             hipStreamSynchronize(c->d2h_stream) == hipSuccess;
+  mark(8);
+  if (trace)
+    fprintf(stderr, "cons_trace fresh=%d resident=%d pool_started=%.1f h2d_rows_issued=%.1f commit_issued=%.1f "
+            "bottom_touched=%.1f bottom_dma_issued=%.1f pool_done=%.1f done_event=%.1f synced=%.1f\n",
+            (int)fresh, (int)resident, tr[1], tr[2], tr[3], tr[4], tr[5], tr[6], tr[7], tr[8]);
   if (fail) {
     if (frc == CDA_OK) {
       c->last_err = std::string("consensus path: ") + fail + ": " + hipGetErrorString(hipGetLastError());
