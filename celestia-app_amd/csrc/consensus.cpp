@@ -271,9 +271,10 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // The caller holds the context lock.  One block of width k (k <= 256): ods host (k^2 x 512), eds_or_null host
 // (4k^2 x 512), roots / dah / err as cda_extend_commit_batch.
 //
-// Input: the ODS goes up in one pageable hipMemcpyAsync (the runtime pins the caller's written pages on the fly):
-// roots-only 0.467 ms per block, against 0.553 ms in four bands (each pageable copy pays its own setup) and 0.59 ms
-// staged through a pinned slab by the copy pool (profiles/r04_pass2.log).  Output, by what the caller's EDS buffer is:
+// Input: pageable hipMemcpyAsync (the runtime pins the caller's written pages on the fly).  Roots only: one copy,
+// 0.467 ms per block, against 0.553 ms in four bands (each pageable copy pays its own setup) and 0.59 ms staged
+// through a pinned slab by the copy pool (profiles/r04_pass2.log).  With the EDS: four bands, so that the first
+// band's Q1 goes down while the rest comes up.  Output, by what the caller's EDS buffer is:
 //   pinned      Q1 and the bottom half straight to it by DMA;
 //   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
 //               pages cheaply and runs at the link rate;
@@ -288,7 +289,7 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // faster than the pageable DMA (r04_pass4.log).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
-  static const int in_mode = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 2;
+  static const int in_mode_env = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : -1;
   static const int out_mode = getenv("CDA_CONS_OUT") ? atoi(getenv("CDA_CONS_OUT")) : 0;
   static const bool trace = getenv("CDA_CONS_TRACE") != nullptr;  // host-side phase timestamps on stderr (A/B runs)
   double tr[10] = {0};
@@ -309,8 +310,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)))
     return rc;
   const bool in_pinned = pinned_host(ods);
-  const bool stage_in = !in_pinned && in_mode == 0;
   const bool want = eds_or_null != nullptr;
+  // input in four bands when the EDS comes back (Q1's D2H of the first band overlaps the rest of the H2D: reused
+  // 0.73 vs 0.76-0.78 ms, fresh 0.90 vs 1.01 ms), whole otherwise (roots only 0.47 vs 0.52 ms; r04_pass5.log)
+  const int in_mode = in_mode_env >= 0 ? in_mode_env : (want ? 1 : 2);
+  const bool stage_in = !in_pinned && in_mode == 0;
   const bool out_pinned = want && pinned_host(eds_or_null);
   bool resident = false;  // output form (pinned / resident / fresh), see above
   if (want && !out_pinned) resident = out_mode == 2 || (out_mode != 1 && pages_resident(eds_or_null, eds_b));
