@@ -346,7 +346,8 @@ def pmc_counters(kernel, B):
     MI355X_MICROARCH.md); valu_insts = SQ_INSTS_VALU (wave-instructions).  The NMT levels kernel runs
     with several grid sizes per step; summaries from round 4 on split its dispatches by grid
     ("nmt_levels_kernel@grid=N"): the largest grid is levels 1-2 (nmt_levels_1), the others the upper
-    levels (nmt_levels, averaged per launch).  None if not covered."""
+    levels (nmt_levels, averaged per launch); the FF8 encoder's two launches likewise (columns: the larger grid).
+    None if not covered."""
     import glob
     import re
 
@@ -379,6 +380,12 @@ def pmc_counters(kernel, B):
                      for key in ("hbm_bytes_corrected", "SQ_INSTS_VALU") if all(key in v for v in rest)}
                 c["bench_batch"] = rest[0].get("bench_batch", PMC_BATCH)
                 src = "nmt_levels_kernel@grid<" + str(g[0][0])
+        elif kernel in ("rs_encode8_rows", "rs_encode8_cols"):
+            g = per_grid(d, "rs_encode8_g2_kernel<7>")  # columns: twice the rows' workgroups (2k codewords)
+            if len(g) != 2:
+                continue
+            c, src = g[0 if kernel == "rs_encode8_cols" else 1][1], \
+                f"rs_encode8_g2_kernel<7>@grid={g[0 if kernel == 'rs_encode8_cols' else 1][0]}"
         else:
             return None
         if not c:

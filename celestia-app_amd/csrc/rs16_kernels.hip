@@ -877,6 +877,9 @@ namespace h2 {
 #ifndef CDA_RS16_H2_STAGGER
 #define CDA_RS16_H2_STAGGER 0
 #endif
+#ifndef CDA_RS16_H2_SPLIT
+#define CDA_RS16_H2_SPLIT 0  // A/B builds: static split of the items by dispatch age (numerator over 8), no queue
+#endif
 #ifndef CDA_RS16_H2_TRACE
 #define CDA_RS16_H2_TRACE 0  // diagnostic builds: s_memrealtime at 4 phases of the first 8 items of each workgroup
 #endif
@@ -1107,12 +1110,23 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int* s_item) {
   if (bid >= G / 2)
     for (int i = 0; i < CDA_RS16_H2_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
 #endif
+#if CDA_RS16_H2_SPLIT > 0
+  // static split by dispatch age: the first G/2 workgroups (one per CU) take SPLIT/8 of the items
+  (void)s_item, (void)lo, (void)hi_item;
+  const int nf = G / 2, fast = bid < nf;
+  const int nF = (int)((long long)a.total * CDA_RS16_H2_SPLIT / 8);
+  const int pool_lo = fast ? 0 : nF, pool_n = fast ? nF : a.total - nF, nw = fast ? nf : G - nf;
+  const int me = fast ? bid : bid - nf;
+  for (int it = 0, t = me; t < pool_n; t += nw, it++) {
+    const int g = pool_lo + t;
+#else
   for (int it = 0;; it++) {
     if (threadIdx.x == 0) *s_item = lo + atomicAdd(&a.queue[part], 1);
     __syncthreads();  // (the previous item's reads of *s_item all precede its exchanges' barriers)
     const int g = *s_item;
     if constexpr (kMode == 1) __syncthreads();  // no exchange barriers follow in the memory-only diagnostic
     if (g >= hi_item) break;
+#endif
     h2_mark(a, w, it, 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) asm volatile("" : "+v"(cx.lv[i]), "+v"(cx.lm[i]));
@@ -1197,7 +1211,7 @@ __device__ __forceinline__ void body(const Args& a, uint4* xb, int* s_item) {
     h2_mark(a, w, it, 3);
   }
   // the last workgroup out leaves the counters zero for the next launch on this stream
-  if (threadIdx.x == 0 && atomicAdd(&a.queue[8], 1) == G - 1) {
+  if (CDA_RS16_H2_SPLIT == 0 && threadIdx.x == 0 && atomicAdd(&a.queue[8], 1) == G - 1) {
     __threadfence();
 #pragma unroll
     for (int i = 0; i < 9; i++) __hip_atomic_store(&a.queue[i], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1259,7 +1273,7 @@ int rs16_reg_init(int device) {
 }
 
 #ifndef CDA_RS16_H2
-#define CDA_RS16_H2 1  // 0: the whole-codeword kernel (same-box A/B builds)
+#define CDA_RS16_H2 0  // 1: the half-slice kernel (A/B builds; measured slower)
 #endif
 
 // The half-slice kernel's item counters, one set per (device, stream): launches on one stream run in order and the
