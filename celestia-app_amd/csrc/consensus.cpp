@@ -125,23 +125,22 @@ class CopyPool {
 };
 
 struct Consensus {
-  static constexpr int kMaxBands = 8, kMaxChunks = 16;
+  static constexpr int kMaxBands = 4, kMaxPieces = 16;
   CopyPool* pool = nullptr;
-  uint8_t* pin_in = nullptr;   // ODS staging (k^2 x 512)
-  uint8_t* pin_out = nullptr;  // Q1 (k x k shares) | bottom half (k x 2k shares)
+  uint8_t* pin_out = nullptr;  // Q1 (k x k shares) of a pageable output
   uint8_t* pin_res = nullptr;  // 4k root records | DAH | status
-  size_t cap_in = 0, cap_out = 0, cap_res = 0;
+  uint8_t* d_res = nullptr;    // the same on the device: one D2H of the results
+  size_t cap_out = 0, cap_res = 0, cap_dres = 0;
   hipEvent_t ev_in[kMaxBands] = {}, ev_rows[kMaxBands] = {}, ev_q1[kMaxBands] = {}, ev_cols = nullptr,
-             ev_bot[kMaxChunks] = {}, ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr;
+             ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr;
   ~Consensus() {
     delete pool;
-    for (uint8_t* p : {pin_in, pin_out, pin_res})
+    for (uint8_t* p : {pin_out, pin_res})
       if (p) (void)hipHostFree(p);
+    if (d_res) (void)hipFree(d_res);
     for (int i = 0; i < kMaxBands; i++)
       for (hipEvent_t e : {ev_in[i], ev_rows[i], ev_q1[i]})
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : ev_bot)
-      if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_cols, ev_done, ev_h2d_end, ev_d2h_end})
       if (e) (void)hipEventDestroy(e);
   }
@@ -175,6 +174,16 @@ int grow_pinned(cda_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
   cap = need;
   return CDA_OK;
 }
+int grow_device(cda_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
+  if (cap >= need) return CDA_OK;
+  fault_point("alloc");
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (!dev_ok(c, hipMalloc((void**)&p, need), "hipMalloc")) return CDA_E_DEVICE;
+  cap = need;
+  return CDA_OK;
+}
 
 int get_consensus(cda_ctx* c, Consensus*& out) {
   if (!c->cons) {
@@ -184,8 +193,6 @@ int get_consensus(cda_ctx* c, Consensus*& out) {
       ok = hipEventCreateWithFlags(&s->ev_in[i], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&s->ev_rows[i], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&s->ev_q1[i], hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; i < Consensus::kMaxChunks && ok; i++)
-      ok = hipEventCreateWithFlags(&s->ev_bot[i], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&s->ev_cols, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->ev_h2d_end, hipEventDisableTiming) == hipSuccess &&
@@ -272,27 +279,27 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // (4k^2 x 512), roots / dah / err as cda_extend_commit_batch.
 //
 // Input: pageable hipMemcpyAsync (the runtime pins the caller's written pages on the fly).  Roots only: one copy,
-// 0.467 ms per block, against 0.553 ms in four bands (each pageable copy pays its own setup) and 0.59 ms staged
+// 0.467 ms per block, against 0.553 ms in four bands (each pageable copy pays its own set-up) and 0.59 ms staged
 // through a pinned slab by the copy pool (profiles/r04_pass2.log).  With the EDS: four bands, so that the first
-// band's Q1 goes down while the rest comes up.  Output, by what the caller's EDS buffer is:
+// band's Q1 goes down while the rest comes up (reused output 0.73 vs 0.76-0.78 ms, r04_pass5.log).
+// Output, by what the caller's EDS buffer is:
 //   pinned      Q1 and the bottom half straight to it by DMA;
 //   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
-//               pages cheaply and runs at the link rate;
-//   fresh       huge pages asked for and every page first touched by the pool (one 2 MiB page per task, the tasks
-//               of distinct pages first) while the device works, then the resident form: a pageable DMA into
-//               never-touched memory faults it page by page in one thread (3.6 ms per block, r04_pass1), and the
-//               earlier fresh form that sent the bottom half through the pinned slab in 1 MiB chunks copied out by
-//               the pool took 1.02-1.23 ms against 0.80-0.88 ms for this one (r04_pass4.log).
-// Q0 is always the host copy of the caller's shares.  CDA_CONS_IN=0 stages the input through the pool, 1 sends it in
-// four bands; CDA_CONS_OUT=1 takes the staged fresh form, 2 forces the resident form on any buffer (A/B
-// runs).  Registering the bottom half (hipHostRegister, plain async DMA, unregistered before returning) measured no
-// faster than the pageable DMA (r04_pass4.log).
+//               pages cheaply and runs near the link rate;
+//   fresh       huge pages asked for and every page first touched by the pool (one 2 MiB range per task) while the
+//               device works, then the resident form with the bottom half in four pieces, each sent once its pages
+//               are touched.  A pageable DMA into never-touched memory faults it page by page in one thread (3.6 ms
+//               per block, r04_pass1); sending the bottom half through the pinned slab in 1 MiB chunks copied out by
+//               the pool took 1.02-1.23 ms against 0.80-0.88 ms for this form (r04_pass4.log); registering it
+//               (hipHostRegister, async DMA, unregister) was no faster.
+// Q0 is always the host copy of the caller's shares.  A/B knobs (read once per process): CDA_CONS_IN = 1 (bands) /
+// 2 (one copy), CDA_CONS_OUT = 2 (the resident form on any pageable buffer), CDA_CONS_TRACE (phase timestamps).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
-  static const int in_mode_env = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : -1;
+  static const int in_mode_env = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 0;
   static const int out_mode = getenv("CDA_CONS_OUT") ? atoi(getenv("CDA_CONS_OUT")) : 0;
-  static const bool trace = getenv("CDA_CONS_TRACE") != nullptr;  // host-side phase timestamps on stderr (A/B runs)
-  double tr[10] = {0};
+  static const bool trace = getenv("CDA_CONS_TRACE") != nullptr;
+  double tr[8] = {0};
   const auto t_start = std::chrono::steady_clock::now();
   auto mark = [&](int i) {
     if (trace) tr[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_start).count();
@@ -305,73 +312,47 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   Consensus* X = nullptr;
   int rc;
   if ((rc = ensure_pipeline(c)) || (rc = get_consensus(c, X)) || (rc = ensure(c, c->ods, ods_b)) ||
-      (rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->roots, roots_b)) || (rc = ensure(c, c->dah, 32)) ||
-      (rc = ensure(c, c->status, 8)) || (rc = ensure(c, c->leaf, cells * CDA_REC_BYTES)) ||
+      (rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->leaf, cells * CDA_REC_BYTES)) ||
       (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)))
     return rc;
-  const bool in_pinned = pinned_host(ods);
   const bool want = eds_or_null != nullptr;
-  // input in four bands when the EDS comes back (Q1's D2H of the first band overlaps the rest of the H2D: reused
-  // 0.73 vs 0.76-0.78 ms, fresh 0.90 vs 1.01 ms), whole otherwise (roots only 0.47 vs 0.52 ms; r04_pass5.log)
-  const int in_mode = in_mode_env >= 0 ? in_mode_env : (want ? 1 : 2);
-  const bool stage_in = !in_pinned && in_mode == 0;
   const bool out_pinned = want && pinned_host(eds_or_null);
-  bool resident = false;  // output form (pinned / resident / fresh), see above
-  if (want && !out_pinned) resident = out_mode == 2 || (out_mode != 1 && pages_resident(eds_or_null, eds_b));
+  const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
-  const bool fresh_direct = fresh && out_mode != 1;  // touched by the pool, then the resident form
-  if ((stage_in && (rc = grow_pinned(c, X->pin_in, X->cap_in, ods_b))) ||
-      (want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + bot_b))) ||
-      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)))
+  const bool banded = in_mode_env ? in_mode_env == 1 : want;
+  if ((want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b))) ||
+      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
     return rc;
   if (fresh) want_huge_pages(eds_or_null, eds_b);
-
-  // bands of the row pass (an even number of rows each: the FF8 encoder takes codeword pairs) and chunks of the
-  // bottom half's copy-out
-  const uint32_t nband = (k >= 16 && in_mode != 2) ? 4 : 1, kb = k / nband;
-  const uint32_t nchunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(Consensus::kMaxChunks, bot_b >> 20));
-  const uint8_t* src_in = stage_in ? X->pin_in : ods;
   uint8_t* d_ods = (uint8_t*)c->ods.p;
   uint8_t* d_eds = (uint8_t*)c->eds.p;
-  uint8_t* pin_q1 = X->pin_out;
-  uint8_t* pin_bot = X->pin_out ? X->pin_out + q1_b : nullptr;
+  uint8_t* d_roots = X->d_res;
+  uint8_t* d_dah = X->d_res + roots_b;
+  auto* d_status = (unsigned long long*)(X->d_res + roots_b + 32);
 
-  std::atomic<bool> abort{false};
-  std::atomic<int> staged[Consensus::kMaxBands];
-  std::atomic<int> q1_rec{0}, bot_rec{0};
-  // fresh output: the bottom half goes down in n_piece pieces (two huge pages each), each DMA'd once the pool has
-  // touched its pages, so the DMA of the first pieces overlaps the faults of the later ones
-  std::atomic<int> touched[Consensus::kMaxChunks];
+  // row-pass bands (an even number of rows each: the FF8 encoder takes codeword pairs); bottom-half pieces of a fresh
+  // output (two huge pages each), each sent once the pool has touched its pages
+  const uint32_t nband = (banded && k >= 16) ? Consensus::kMaxBands : 1, kb = k / nband;
   const int n_touch = fresh ? (int)std::max<size_t>(1, bot_b >> 21) : 0;
-  const int n_piece = fresh_direct ? std::min(Consensus::kMaxChunks, std::max(1, n_touch / 2)) : 1;
-  for (int p = 0; p < Consensus::kMaxChunks; p++) touched[p].store(0);
-  const size_t band_b = (size_t)kb * rowS;
-  const int pieces_per_band = band_b >= ((size_t)1 << 20) ? 4 : 1;
-  for (uint32_t b = 0; b < nband; b++) staged[b].store(stage_in ? pieces_per_band : 0);
+  const int n_piece = fresh ? std::min(Consensus::kMaxPieces, std::max(1, n_touch / 2)) : 1;
+  std::atomic<bool> abort{false};
+  std::atomic<int> q1_rec{0};
+  std::atomic<int> touched[Consensus::kMaxPieces];
+  for (int p = 0; p < Consensus::kMaxPieces; p++) touched[p].store(0);
 
   std::vector<std::function<void()>> tasks;
-  tasks.reserve(128);
-  if (stage_in)  // ODS rows -> pinned slab, band by band
-    for (uint32_t b = 0; b < nband; b++)
-      for (int q = 0; q < pieces_per_band; q++) {
-        const size_t lo = b * band_b + band_b * q / pieces_per_band, hi = b * band_b + band_b * (q + 1) / pieces_per_band;
-        tasks.emplace_back([=, &staged] {
-          memcpy(X->pin_in + lo, ods + lo, hi - lo);
-          staged[b].fetch_sub(1, std::memory_order_acq_rel);
-        });
-      }
+  tasks.reserve(64);
   if (want) {
-    if (fresh)  // first touch of the bottom half while the device works: one 2 MiB range (a huge page) per task
-      for (int j = 0; j < n_touch; j++) {
-        const size_t lo = bot_b * j / n_touch, hi = bot_b * (j + 1) / n_touch;
-        const int piece = j * n_piece / n_touch;
-        tasks.emplace_back([=, &touched] {
-          touch_pages(eds_or_null + k * erowS + lo, hi - lo);
-          touched[piece].fetch_add(1, std::memory_order_acq_rel);
-        });
-      }
+    for (int j = 0; j < n_touch; j++) {  // first touch of a fresh bottom half, one 2 MiB range per task
+      const size_t lo = bot_b * j / n_touch, hi = bot_b * (j + 1) / n_touch;
+      const int piece = j * n_piece / n_touch;
+      tasks.emplace_back([=, &touched] {
+        touch_pages(eds_or_null + k * erowS + lo, hi - lo);
+        touched[piece].fetch_add(1, std::memory_order_acq_rel);
+      });
+    }
     // Q0 = the shares, host to host (and the first touch of each row's Q1 half); a task covers 1 MiB of EDS rows at
-    // k = 128, and the even tasks go first so that the first faults land on distinct huge pages
+    // k = 128, the even tasks first so that the first faults land on distinct huge pages
     const uint32_t rows_per_task = std::max<uint32_t>(1, (uint32_t)(((size_t)512 << 10) / rowS));
     const uint32_t n_q0 = (k + rows_per_task - 1) / rows_per_task;
     for (uint32_t half = 0; half < 2; half++)
@@ -390,33 +371,21 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
           tasks.emplace_back([=, &q1_rec, &abort] {
             if (!wait_count(q1_rec, (int)b + 1, abort) || !wait_event(X->ev_q1[b], abort)) return;
             for (uint32_t r = r0; r < std::min((b + 1) * kb, r0 + rows_per_task); r++)
-              memcpy(eds_or_null + r * erowS + rowS, pin_q1 + r * rowS, rowS);
+              memcpy(eds_or_null + r * erowS + rowS, X->pin_out + r * rowS, rowS);
           });
-    if (fresh && !fresh_direct)
-      for (uint32_t j = 0; j < nchunk; j++) {  // bottom-half chunk j (1 MiB at k = 128), four tasks each: the last
-                                               // chunk's host copy is on the critical path
-        const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
-        for (int h = 0; h < 4; h++) {
-          const size_t a = lo + (hi - lo) * h / 4, z = lo + (hi - lo) * (h + 1) / 4;
-          tasks.emplace_back([=, &bot_rec, &abort] {
-            if (!wait_count(bot_rec, (int)j + 1, abort) || !wait_event(X->ev_bot[j], abort)) return;
-            memcpy(eds_or_null + k * erowS + a, pin_bot + a, z - a);
-          });
-        }
-      }
   }
   X->pool->start(&tasks);
   mark(1);
 
-  // device work, issued band by band as the input lands
   hipStream_t s = c->stream;
   const char* fail = nullptr;
   int frc = CDA_OK;
-  for (uint32_t b = 0; b < nband && !fail; b++) {
+  // the order-status word is set on the compute stream while the input is still coming up (off the chain)
+  if (hipMemsetAsync(d_status, 0xFF, 8, s) != hipSuccess) fail = "status";
+  for (uint32_t b = 0; b < nband && !fail; b++) {  // device work, band by band as the input lands
     const size_t r0 = (size_t)b * kb;
-    while (staged[b].load(std::memory_order_acquire) > 0) std::this_thread::yield();  // the pool staged band b
-    if (hipMemcpyAsync(d_ods + r0 * rowS, src_in + r0 * rowS, band_b, hipMemcpyHostToDevice, c->h2d_stream) !=
-            hipSuccess ||
+    if (hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
+                       c->h2d_stream) != hipSuccess ||
         hipEventRecord(X->ev_in[b], c->h2d_stream) != hipSuccess || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
       fail = "H2D";
       break;
@@ -432,7 +401,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       break;
     }
     if (want) {
-      uint8_t* dst = out_pinned ? eds_or_null + r0 * erowS + rowS : pin_q1 + r0 * rowS;
+      uint8_t* dst = out_pinned ? eds_or_null + r0 * erowS + rowS : X->pin_out + r0 * rowS;
       const size_t dpitch = out_pinned ? erowS : rowS;
       if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
           hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
@@ -453,42 +422,31 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       fail = "cols";
     }
   }
-  if (!fail && want) {
-    if (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess)
-      fail = "event";
-    for (uint32_t j = 0; j < nchunk && !fail && !resident && !fresh_direct; j++) {
-      const size_t lo = bot_b * j / nchunk, hi = bot_b * (j + 1) / nchunk;
-      uint8_t* dst = out_pinned ? eds_or_null + k * erowS + lo : pin_bot + lo;
-      if (hipMemcpyAsync(dst, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
-          hipEventRecord(X->ev_bot[j], c->d2h_stream) != hipSuccess) {
-        fail = "bottom D2H";
-        break;
-      }
-      bot_rec.store((int)j + 1, std::memory_order_release);
-    }
-  }
+  if (!fail && want &&
+      (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess))
+    fail = "event";
+  if (!fail && out_pinned &&
+      hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
+          hipSuccess)
+    fail = "bottom D2H";
   if (!fail) {
-    if ((rc = enqueue_commit(c, k, 1, d_eds, c->roots.p, c->dah.p, (unsigned long long*)c->status.p, s, 0))) {
+    if ((rc = enqueue_commit(c, k, 1, d_eds, d_roots, d_dah, d_status, s, 0, false))) {
       frc = rc;
       fail = "commit";
-    } else if (hipMemcpyAsync(X->pin_res, c->roots.p, roots_b, hipMemcpyDeviceToHost, s) != hipSuccess ||
-               hipMemcpyAsync(X->pin_res + roots_b, c->dah.p, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
-               hipMemcpyAsync(X->pin_res + roots_b + 32, c->status.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    } else if (hipMemcpyAsync(X->pin_res, X->d_res, res_b, hipMemcpyDeviceToHost, s) != hipSuccess ||
                hipEventRecord(X->ev_done, s) != hipSuccess) {
       fail = "results D2H";
     }
   }
   mark(3);
-  // resident output: the bottom half by one pageable DMA (this thread waits in it while the pool copies Q0 / Q1);
-  // fresh_direct: the same once the pool has touched every page of it
-  mark(4);
-  for (int p = 0; p < n_piece && !fail && (resident || fresh_direct); p++) {
-    if (fresh_direct) {  // the touch tasks of piece p: j with j * n_piece / n_touch == p
-      const int need = (int)(((int64_t)(p + 1) * n_touch + n_piece - 1) / n_piece - ((int64_t)p * n_touch + n_piece - 1) / n_piece);
-      while (touched[p].load(std::memory_order_acquire) < need) {
-        if (abort.load(std::memory_order_relaxed)) break;
+  // pageable output: the bottom half by pageable DMA from this thread (it waits in each call while the pool copies
+  // Q0 / Q1); a fresh output piece by piece as the pool finishes touching it
+  for (int p = 0; p < n_piece && !fail && want && !out_pinned; p++) {
+    if (fresh) {  // the touch tasks of piece p: j with j * n_piece / n_touch == p
+      const int need = (int)(((int64_t)(p + 1) * n_touch + n_piece - 1) / n_piece -
+                             ((int64_t)p * n_touch + n_piece - 1) / n_piece);
+      while (touched[p].load(std::memory_order_acquire) < need && !abort.load(std::memory_order_relaxed))
         std::this_thread::yield();
-      }
     }
     const size_t lo = bot_b * p / n_piece, hi = bot_b * (p + 1) / n_piece;
     if (hipMemcpyAsync(eds_or_null + k * erowS + lo, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost,
@@ -498,12 +456,12 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   if (!fail && (hipEventRecord(X->ev_h2d_end, c->h2d_stream) != hipSuccess ||
                 hipEventRecord(X->ev_d2h_end, c->d2h_stream) != hipSuccess))
     fail = "event";
-  mark(5);
+  mark(4);
   if (fail) abort.store(true);
   X->pool->help_and_wait();
-  mark(6);
+  mark(5);
   if (!fail) wait_event(X->ev_done, abort);
-  mark(7);
+  mark(6);
   // every DMA of this call has finished before the caller's buffers (or the staging) can be touched again: the
   // streams' end events (a stream sync costs ~6 us per stream here), or whole-stream syncs after a failure
   bool synced;
@@ -512,11 +470,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   else
     synced = hipStreamSynchronize(c->h2d_stream) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
              hipStreamSynchronize(c->d2h_stream) == hipSuccess;
-  mark(8);
+  mark(7);
   if (trace)
-    fprintf(stderr, "cons_trace fresh=%d resident=%d pool_started=%.1f h2d_rows_issued=%.1f commit_issued=%.1f "
-            "bottom_touched=%.1f bottom_dma_issued=%.1f pool_done=%.1f done_event=%.1f synced=%.1f\n",
-            (int)fresh, (int)resident, tr[1], tr[2], tr[3], tr[4], tr[5], tr[6], tr[7], tr[8]);
+    fprintf(stderr, "cons_trace fresh=%d resident=%d pool_started=%.1f rows_issued=%.1f commit_issued=%.1f "
+            "bottom_dma_issued=%.1f pool_done=%.1f done_event=%.1f synced=%.1f\n",
+            (int)fresh, (int)resident, tr[1], tr[2], tr[3], tr[4], tr[5], tr[6], tr[7]);
   if (fail) {
     if (frc == CDA_OK) {
       c->last_err = std::string("consensus path: ") + fail + ": " + hipGetErrorString(hipGetLastError());

@@ -131,9 +131,10 @@ void free_consensus(cda_ctx* c);
 // RS jobs of the block path: rows (ODS row r -> Q0 copy + Q1 row r) and columns (top half -> bottom half)
 RsJob rows_job(uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds);
 RsJob cols_job(uint32_t k, uint32_t nblocks, uint8_t* d_eds);
-// commitment phase (leaf hashing, NMT levels, DAH) of nblocks extended blocks in d_eds on stream s
+// commitment phase (leaf hashing, NMT levels, DAH) of nblocks extended blocks in d_eds on stream s; the order-status
+// words are set to "no error" first unless the caller already did (init_status = false)
 int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
-                   unsigned long long* d_status, hipStream_t s, size_t rec_off);
+                   unsigned long long* d_status, hipStream_t s, size_t rec_off, bool init_status = true);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 // split_kernels.hip

@@ -251,8 +251,9 @@ int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void*
 }
 
 int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
-                   unsigned long long* d_status, hipStream_t s, size_t rec_off) {
-  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
+                   unsigned long long* d_status, hipStream_t s, size_t rec_off, bool init_status) {
+  if (init_status && !dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync"))
+    return CDA_E_DEVICE;
   {
     ProfScope ps(c, "leaf_hash", s);
     if (launch_leaf_hash(d_eds, bufs0(c, rec_off), d_status, (int)k, (int)nblocks, s)) return CDA_E_DEVICE;
@@ -271,8 +272,11 @@ int enqueue_pipeline(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_
   if (rc) return rc;
   rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES);  // inner tree levels
   if (rc) return rc;
+  // the order-status words are set before the extension, so no fill sits between the column pass and the leaf
+  // hashing on the dependent chain of a one-block call
+  if (!dev_ok(c, hipMemsetAsync(d_status, 0xFF, (size_t)nblocks * 8, s), "hipMemsetAsync")) return CDA_E_DEVICE;
   if ((rc = enqueue_rs(c, k, nblocks, d_ods, d_eds, s))) return rc;
-  return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, 0);
+  return enqueue_commit(c, k, nblocks, d_eds, d_roots, d_dah, d_status, s, 0, false);
 }
 
 // 96-B records -> packed 90-B nodes
