@@ -292,13 +292,14 @@ void want_huge_pages(uint8_t* p, size_t n) {
 //               per block, r04_pass1); sending the bottom half through the pinned slab in 1 MiB chunks copied out by
 //               the pool took 1.02-1.23 ms against 0.80-0.88 ms for this form (r04_pass4.log); registering it
 //               (hipHostRegister, async DMA, unregister) was no faster.
-// Q0 is always the host copy of the caller's shares.  A/B knobs (read once per process): CDA_CONS_IN = 1 (bands) /
+// Q0 is always the host copy of the caller's shares.  A/B knobs (read per call): CDA_CONS_IN = 1 (bands) /
 // 2 (one copy), CDA_CONS_OUT = 2 (the resident form on any pageable buffer), CDA_CONS_TRACE (phase timestamps).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
-  static const int in_mode_env = getenv("CDA_CONS_IN") ? atoi(getenv("CDA_CONS_IN")) : 0;
-  static const int out_mode = getenv("CDA_CONS_OUT") ? atoi(getenv("CDA_CONS_OUT")) : 0;
-  static const bool trace = getenv("CDA_CONS_TRACE") != nullptr;
+  const char* e_in = getenv("CDA_CONS_IN");  // read per call: the tests switch forms within one process
+  const char* e_out = getenv("CDA_CONS_OUT");
+  const int in_mode_env = e_in ? atoi(e_in) : 0, out_mode = e_out ? atoi(e_out) : 0;
+  const bool trace = getenv("CDA_CONS_TRACE") != nullptr;
   double tr[8] = {0};
   const auto t_start = std::chrono::steady_clock::now();
   auto mark = [&](int i) {

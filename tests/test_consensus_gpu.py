@@ -1,8 +1,9 @@
 """The one-block host-buffer path (csrc/consensus.cpp): cda_extend_commit / cda_extend_commit_batch with one block,
 as PrepareProposal / ProcessProposal call da.ExtendShares (app/prepare_proposal.go:65-93,
-app/process_proposal.go:137-151).  Row bands staged through pinned slabs by a copy pool, Q0 copied host to host,
-Q1 / the bottom half copied back while the device hashes.  Every case is bit-exact against the oracle, and against
-the serial form (a context opened with CDA_CONSENSUS=0) for the error reports."""
+app/process_proposal.go:137-151).  The input goes up in row bands (or one copy for roots only), Q0 is copied host to
+host by a copy pool, Q1 and the bottom half come back while the device hashes, and the output form follows the
+caller's buffer (pinned / written before / fresh and untouched).  Every case is bit-exact against the oracle, and
+against the serial form (a context opened with CDA_CONSENSUS=0) for the error reports."""
 import threading
 
 import numpy as np
@@ -47,6 +48,23 @@ def test_one_block_fresh_buffers(ctx, k, want_eds):
     ods = O.gen_ods(k, 0xC0DE + k)
     eds, rr, cr, dah = ctx.extend_commit(ods.copy(), want_eds=want_eds)
     _check(ods, eds, rr, cr, dah, want_eds)
+
+
+@pytest.mark.parametrize("cons_in,cons_out", [("1", "0"), ("2", "0"), ("1", "2"), ("2", "2")])
+@pytest.mark.parametrize("k", [16, 128])
+@pytest.mark.parametrize("buf", ["fresh", "written"])
+def test_one_block_forms(ctx, monkeypatch, cons_in, cons_out, k, buf):
+    """Every input form (CDA_CONS_IN: four bands / one copy) with every pageable output form (CDA_CONS_OUT=0: chosen
+    by residency -- fresh buffers are touched by the pool and sent in pieces; 2: the written-buffer form forced, so
+    the runtime faults a fresh buffer in itself), fresh and written output buffers."""
+    monkeypatch.setenv("CDA_CONS_IN", cons_in)
+    monkeypatch.setenv("CDA_CONS_OUT", cons_out)
+    ods = O.gen_ods(k, 0xF0F0 + k)
+    out = np.empty((1, 4 * k * k, 512), np.uint8) if buf == "fresh" else np.full((1, 4 * k * k, 512), 0x3C, np.uint8)
+    eds, rr, cr, dah = ctx.extend_commit_batch(ods[None].copy(), eds_out=out)
+    _check(ods, out[0], rr[0], cr[0], dah[0])
+    _, rr2, cr2, dah2 = ctx.extend_commit_batch(ods[None].copy(), want_eds=False)
+    assert np.array_equal(rr2, rr) and np.array_equal(cr2, cr) and bytes(dah2[0]) == bytes(dah[0])
 
 
 @pytest.mark.parametrize("k", [64, 128])
