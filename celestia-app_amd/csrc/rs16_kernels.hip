@@ -41,10 +41,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-#include <map>
-#include <mutex>
-#include <utility>
-
 #include "cda_internal.h"
 #include "gf16_const.h"
 #include "gf_slice.h"
@@ -396,8 +392,6 @@ struct Args {
   long long cpy_blk, cpy_cw, cpy_sh;
   const uint16_t* cpoly;
   int cw_per_blk, slices, total;  // total = codewords of the launch
-  unsigned long long* trace;      // diagnostic builds (CDA_RS16_H2_TRACE): per-workgroup phase timestamps
-  int* queue;                     // half-slice kernel: per-partition item counters + a done counter (zero at launch)
 };
 
 // Diagnostic builds only (scripts/gpu_rs16_diag.sh compiles a separate library with -DCDA_RS16_DIAG_MODE=N):
@@ -854,387 +848,6 @@ __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   }
 }
 
-
-// ---- half-slice form: two workgroups per CU (round 4) --------------------------------------------------------------
-// The whole-codeword kernel above fills a CU's registers with one codeword, so its loads and stores never overlap
-// another workgroup's compute: memory-only 0.116 ms and compute-only 0.138 ms per column square add up to the
-// product's 0.27 (profiles/r04_rs16_diag.log).  Here a work item is HALF of every shard's 512-B slice (the FFT is
-// over positions, element by element, so the two 256-B halves are independent codewords of the same transform):
-// 512 positions x 256 B = 128 KiB = 8 waves x 64 lanes x 64 VGPRs, and a CU holds two such workgroups, one
-// computing while the other loads or stores (the FF8 encoder's arrangement).
-//   lane bits 0..1 = unit u (four lanes cover the 256-B half of a shard: pair_in's chunks at u*16 + 64q),
-//   lane bits 2..5 = four position bits, register bits R0, R1 = two, wave bits W0..W2 = three.
-//   LA  p0:R0 p1:R1 p2:L5 p3:L4 p4:L3 p5:L2 p6..p8:W0..W2   IFFT d = 0, 1 (load)  / FFT d = 1, 0 (store)
-//   LB  p2:R0 p3:R1 p0:L5 p1:L4                           IFFT d = 2, 3         / FFT d = 3, 2   (swap_lane45)
-//   LC  p4:R0 p5:R1 p2:L3 p3:L2                           IFFT d = 4, 5         / FFT d = 5, 4   (lane ^ 8, ^ 4)
-//   LD  p6:R0 p7:R1 p4:W0 p5:W1                           IFFT d = 6, 7         / FFT d = 7, 6   (LDS, 2 bits)
-//   LE  p8:R0 p6:W2                                       IFFT d = 8, FFT d = 8                  (LDS, 1 bit)
-// Every wave bit is compile-time (one body per wave), so layers 4..8 multiply by compile-time constants; layers 2, 3
-// have two lane bits above them (p4, p5): the affine split, two lane-masked XOR programs; layers 0, 1 (four lane bits
-// above) use the generic per-lane multiply with preloaded constants, as the whole-codeword kernel.
-namespace h2 {
-
-#ifndef CDA_RS16_H2_STAGGER
-#define CDA_RS16_H2_STAGGER 0
-#endif
-#ifndef CDA_RS16_H2_SPLIT
-#define CDA_RS16_H2_SPLIT 0  // A/B builds: static split of the items by dispatch age (numerator over 8), no queue
-#endif
-#ifndef CDA_RS16_H2_TRACE
-#define CDA_RS16_H2_TRACE 0  // diagnostic builds: s_memrealtime at 4 phases of the first 8 items of each workgroup
-#endif
-// trace[(bid * 8 + item) * 4 + phase], phase 0 = loop top, 1 = state built (loads consumed), 2 = transforms done,
-// 3 = stores issued; written by lane 0 of wave 0 with a vector store
-__device__ __forceinline__ void h2_mark(const Args& a, int w, int it, int ph) {
-#if CDA_RS16_H2_TRACE
-  if (w == 0 && it < 8) {
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    if ((threadIdx.x & 63) == 0) a.trace[((size_t)blockIdx.x * 8 + it) * 4 + ph] = t;
-    if (it == 0 && ph == 0 && (threadIdx.x & 63) == 0) {  // where the workgroup runs: XCC_ID << 32 | HW_ID
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-      a.trace[(size_t)gridDim.x * 32 + blockIdx.x] = ((unsigned long long)xcc << 32) | hw;
-    }
-  }
-#else
-  (void)a, (void)w, (void)it, (void)ph;
-#endif
-}
-
-struct Lay {
-  int s[L];  // slot of position bit b: 0, 1 = R0, R1; 2..5 = lane bit; 8, 9, 10 = W0..W2
-};
-constexpr Lay LA{{0, 1, 5, 4, 3, 2, 8, 9, 10}};
-constexpr Lay LB{{5, 4, 0, 1, 3, 2, 8, 9, 10}};
-constexpr Lay LC{{5, 4, 3, 2, 0, 1, 8, 9, 10}};
-constexpr Lay LD{{5, 4, 3, 2, 8, 9, 0, 1, 10}};
-constexpr Lay LE{{5, 4, 3, 2, 8, 9, 10, 1, 0}};
-
-constexpr bool is_lane(int s) { return s >= 2 && s < 8; }
-constexpr int pos_r(const Lay& Y, int r) {
-  int p = 0;
-  for (int b = 0; b < L; b++)
-    if (Y.s[b] < 2 && ((r >> Y.s[b]) & 1)) p |= 1 << b;
-  return p;
-}
-constexpr int pos_w(const Lay& Y, int w) {
-  int p = 0;
-  for (int b = 0; b < L; b++)
-    if (Y.s[b] >= 8 && ((w >> (Y.s[b] - 8)) & 1)) p |= 1 << b;
-  return p;
-}
-__device__ __forceinline__ int pos_lane(const Lay& Y, int lane) {
-  int p = 0;
-#pragma unroll
-  for (int b = 0; b < L; b++)
-    if (is_lane(Y.s[b])) p |= ((lane >> Y.s[b]) & 1) << b;
-  return p;
-}
-constexpr int lane_bits_above(const Lay& Y, int d) {
-  int n = 0;
-  for (int b = d + 1; b < L; b++)
-    if (is_lane(Y.s[b])) n++;
-  return n;
-}
-constexpr int pos_of_slot(const Lay& Y, int slot) {
-  for (int b = 0; b < L; b++)
-    if (Y.s[b] == slot) return b;
-  return -1;
-}
-
-struct Ctx {
-  const uint16_t* cpoly;
-  uint32_t lv[4];  // generic per-lane constants of layers 0, 1 (r16::lv_slot)
-  uint32_t lm[4];  // all-ones in lanes with lane bit 2 + i set
-};
-
-// X ^= t * Y in the lanes whose lane bit SLOT is set, t = g(2^P) ^ g(0) (the affine term of position bit P)
-template <bool INVERSE, int D, const Lay& Y, int SLOT>
-__device__ __forceinline__ void lane_term(uint32_t (&X)[16], const uint32_t (&Yv)[16], const Ctx& cx) {
-  constexpr int P = pos_of_slot(Y, SLOT);
-  if constexpr (P > D) {
-    constexpr unsigned t = kCpoly16[cidx<INVERSE, D>(1 << P)] ^ kCpoly16[cidx<INVERSE, D>(0)];
-    muladd_const_masked<t>(X, Yv, cx.lm[SLOT - 2]);
-  }
-}
-
-template <const Lay& Y, bool INVERSE, int D, int R, int OM>
-__device__ __forceinline__ void butterfly(uint32_t (&E)[4][16], const Ctx& cx) {
-  constexpr int RB = Y.s[D];
-  static_assert(RB == 0 || RB == 1, "butterfly bit must sit in a register slot");
-  if constexpr (!((R >> RB) & 1)) {
-    uint32_t(&X)[16] = E[R];
-    uint32_t(&Yv)[16] = E[R | (1 << RB)];
-    constexpr int hi = ~((2 << D) - 1);
-    if (INVERSE) {
-#pragma unroll
-      for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
-    }
-    if constexpr (lane_bits_above(Y, D) > 2) {  // layers 0, 1: per-lane constant (preloaded), generic multiply
-      constexpr int slot = lv_slot(INVERSE, D, R);
-      muladd_lane(X, Yv, (cx.lv[slot >> 1] >> (16 * (slot & 1))) & 0xFFFFu);
-    } else {  // compile-time (register and wave bits), plus one lane-masked term per lane bit above d
-      constexpr int sct = (pos_r(Y, R) + pos_w(Y, OM)) & hi;
-      static_assert(cidx<INVERSE, D>(sct) < kCpoly16N, "constant table too short");
-      muladd_const<kCpoly16[cidx<INVERSE, D>(sct)]>(X, Yv);
-      lane_term<INVERSE, D, Y, 2>(X, Yv, cx);
-      lane_term<INVERSE, D, Y, 3>(X, Yv, cx);
-      lane_term<INVERSE, D, Y, 4>(X, Yv, cx);
-      lane_term<INVERSE, D, Y, 5>(X, Yv, cx);
-    }
-    if (!INVERSE) {
-#pragma unroll
-      for (int j = 0; j < 16; j++) Yv[j] ^= X[j];
-    }
-  }
-}
-template <const Lay& Y, bool INVERSE, int D, int OM>
-__device__ __forceinline__ void layer(uint32_t (&E)[4][16], const Ctx& cx) {
-  butterfly<Y, INVERSE, D, 0, OM>(E, cx);
-  butterfly<Y, INVERSE, D, 1, OM>(E, cx);
-  butterfly<Y, INVERSE, D, 2, OM>(E, cx);
-  butterfly<Y, INVERSE, D, 3, OM>(E, cx);
-}
-
-template <bool INVERSE, int D, int R, int OM>
-__device__ __forceinline__ void lv_fetch(Ctx& cx, int lane) {
-  constexpr int hi = ~((2 << D) - 1);
-  constexpr int base = INVERSE ? (M - 1 + (pos_r(LA, R) & hi) + (1 << D)) : ((pos_r(LA, R) & hi) + (1 << D) - 1);
-  constexpr int slot = lv_slot(INVERSE, D, R);
-  const uint32_t c = cx.cpoly[base + ((pos_lane(LA, lane) + pos_w(LA, OM)) & hi)];
-  cx.lv[slot >> 1] |= c << (16 * (slot & 1));
-}
-template <int OM>
-__device__ __forceinline__ void lv_fetch_all(Ctx& cx, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) cx.lv[i] = 0;
-  lv_fetch<true, 0, 0, OM>(cx, lane);
-  lv_fetch<true, 0, 2, OM>(cx, lane);
-  lv_fetch<true, 1, 0, OM>(cx, lane);
-  lv_fetch<true, 1, 1, OM>(cx, lane);
-  lv_fetch<false, 1, 0, OM>(cx, lane);
-  lv_fetch<false, 1, 1, OM>(cx, lane);
-  lv_fetch<false, 0, 0, OM>(cx, lane);
-  lv_fetch<false, 0, 2, OM>(cx, lane);
-}
-
-// R1 <-> lane bit 2 (with swap_lane3: LB <-> LC): the partner lane ^ 4 by DPP row_ror:12 (lanes with bit 2 clear,
-// partner l + 4) or row_ror:4 (bit 2 set, partner l - 4), selects on lm = all-ones in lanes with bit 2 set.
-__device__ __forceinline__ uint32_t x4(uint32_t v, uint32_t lm) {
-  const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false);  // row_ror:12
-  const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
-  return sel(lm, dn, up);
-}
-__device__ __forceinline__ void swap_lane2(uint32_t (&E)[4][16], uint32_t lm) {
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t a = E[q][j], b = E[q + 2][j];
-      const uint32_t recv = x4(sel(lm, a, b), lm);
-      E[q][j] = sel(lm, recv, a);
-      E[q + 2][j] = sel(lm, b, recv);
-    }
-  }
-}
-
-// (R0, R1) <-> (W0, W1) through LDS (LC <-> LD), as r16::exchange_w<0> with one other wave bit (W2): thread (w, r)
-// writes key (W2, wp, r), reads key (W2, r, wp); two rounds of 8 planes, 64 KiB.
-__device__ __forceinline__ void exchange2(uint32_t (&E)[4][16], uint4* xb, int w, int lane) {
-  const int wp = w & 3, wo = w >> 2;
-#pragma unroll
-  for (int half = 0; half < 2; half++) {
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      if (r == wp) continue;
-      uint4* p = xb + ((((wo * 4 + wp) * 4 + r) * 2) * 64 + lane);
-      p[0] = make_uint4(E[r][8 * half + 0], E[r][8 * half + 1], E[r][8 * half + 2], E[r][8 * half + 3]);
-      p[64] = make_uint4(E[r][8 * half + 4], E[r][8 * half + 5], E[r][8 * half + 6], E[r][8 * half + 7]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      if (r == wp) continue;
-      const uint4* p = xb + ((((wo * 4 + r) * 4 + wp) * 2) * 64 + lane);
-      const uint4 v0 = p[0], v1 = p[64];
-      E[r][8 * half + 0] = v0.x, E[r][8 * half + 1] = v0.y, E[r][8 * half + 2] = v0.z, E[r][8 * half + 3] = v0.w;
-      E[r][8 * half + 4] = v1.x, E[r][8 * half + 5] = v1.y, E[r][8 * half + 6] = v1.z, E[r][8 * half + 7] = v1.w;
-    }
-    __syncthreads();
-  }
-}
-// R0 <-> W2 through LDS (LD <-> LE): register r = (r1, r0) of wave w = (b = W2, wl = W1 W0) moves iff r0 != b; it
-// writes key (wl, r1, r0) and reads key (wl, r1, b) -- all 16 planes in one round, 16 keys x 4 KiB = 64 KiB.
-__device__ __forceinline__ void exchange1(uint32_t (&E)[4][16], uint4* xb, int w, int lane) {
-  const int b = w >> 2, wl = w & 3;
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    if ((r & 1) == b) continue;
-    uint4* p = xb + ((((wl * 2 + (r >> 1)) * 2 + (r & 1)) * 4) * 64 + lane);
-#pragma unroll
-    for (int c = 0; c < 4; c++) p[c * 64] = make_uint4(E[r][4 * c], E[r][4 * c + 1], E[r][4 * c + 2], E[r][4 * c + 3]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    if ((r & 1) == b) continue;
-    const uint4* p = xb + ((((wl * 2 + (r >> 1)) * 2 + b) * 4) * 64 + lane);
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint4 v = p[c * 64];
-      E[r][4 * c] = v.x, E[r][4 * c + 1] = v.y, E[r][4 * c + 2] = v.z, E[r][4 * c + 3] = v.w;
-    }
-  }
-  __syncthreads();
-}
-
-// 64-B unit of one position of the half slice: chunks q = 0..3 at u*16 + 64q
-template <int OM>
-__device__ __forceinline__ void body(const Args& a, uint4* xb, int* s_item) {
-  constexpr int w = OM;
-  const int lane0 = threadIdx.x & 63;
-  Ctx cx{a.cpoly, {}, {}};
-#pragma unroll
-  for (int i = 0; i < 4; i++) cx.lm[i] = ((lane0 >> (2 + i)) & 1) ? ~0u : 0u;
-  lv_fetch_all<OM>(cx, lane0);
-  // Dynamic item queue.  With a static stride the older workgroup of a CU wins the SIMDs' issue arbitration (it
-  // computed an item in ~27 us, its partner in ~53 us) and finishes first; the other then runs alone on half the
-  // waves (r04 phase trace, scripts/h2_trace_probe.py).  Each workgroup instead takes the next item of its
-  // partition (one per XCD under round-robin dispatch: consecutive items -- the two halves of a shard slice -- are
-  // read through one L2) until the partition is empty, so both workgroups of a CU stay busy to the end.
-  const int G = (int)gridDim.x, bid = (int)blockIdx.x;
-  const int nparts = G < 8 ? G : 8, part = bid % nparts;
-  const int lo = (int)((long long)a.total * part / nparts), hi_item = (int)((long long)a.total * (part + 1) / nparts);
-#if CDA_RS16_H2_STAGGER > 0
-  // A/B builds: start the workgroups of the second half of the grid (the second workgroup of each CU) later, so
-  // that the two workgroups of a CU begin out of phase
-  if (bid >= G / 2)
-    for (int i = 0; i < CDA_RS16_H2_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
-#endif
-#if CDA_RS16_H2_SPLIT > 0
-  // static split by dispatch age: the first G/2 workgroups (one per CU) take SPLIT/8 of the items
-  (void)s_item, (void)lo, (void)hi_item;
-  const int nf = G / 2, fast = bid < nf;
-  const int nF = (int)((long long)a.total * CDA_RS16_H2_SPLIT / 8);
-  const int pool_lo = fast ? 0 : nF, pool_n = fast ? nF : a.total - nF, nw = fast ? nf : G - nf;
-  const int me = fast ? bid : bid - nf;
-  for (int it = 0, t = me; t < pool_n; t += nw, it++) {
-    const int g = pool_lo + t;
-#else
-  for (int it = 0;; it++) {
-    if (threadIdx.x == 0) *s_item = lo + atomicAdd(&a.queue[part], 1);
-    __syncthreads();  // (the previous item's reads of *s_item all precede its exchanges' barriers)
-    const int g = *s_item;
-    if constexpr (kMode == 1) __syncthreads();  // no exchange barriers follow in the memory-only diagnostic
-    if (g >= hi_item) break;
-#endif
-    h2_mark(a, w, it, 0);
-#pragma unroll
-    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(cx.lv[i]), "+v"(cx.lm[i]));
-    int lane = lane0;
-    asm volatile("" : "+v"(lane));
-    const int u = lane & 3;
-    const int pl = pos_lane(LA, lane) + pos_w(LA, w);
-    const SliceMasks km = slice_masks();
-    uint32_t m1 = (lane & 2) ? ~0u : 0u;
-    asm volatile("" : "+v"(m1));
-    const int slice = g % a.slices;
-    const int cw = (g / a.slices) % a.cw_per_blk, blk = (g / a.slices) / a.cw_per_blk;
-    const long long off = (long long)slice * 256 + u * 16;
-    const uint8_t* src = a.src + blk * a.src_blk + cw * a.src_cw + off;
-    uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + off;
-    uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + off : nullptr;
-
-    uint32_t E[4][16];
-    uint4 q[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int sh = pl + pos_r(LA, r);
-      if (kMode < 2) {
-        const uint4* p = reinterpret_cast<const uint4*>(src + sh * a.src_sh);
-        q[r][0] = p[0], q[r][1] = p[4], q[r][2] = p[8], q[r][3] = p[12];
-      } else {  // diagnostic modes >= 2: synthetic data, no loads
-        q[r][0] = make_uint4(sh, lane, w, r), q[r][1] = make_uint4(lane * 3, sh ^ 5, 7, w), q[r][2] = q[r][0];
-        q[r][3] = q[r][1];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      if (cpy) {
-        uint4* o = reinterpret_cast<uint4*>(cpy + (pl + pos_r(LA, r)) * a.cpy_sh);
-        o[0] = q[r][0], o[4] = q[r][1], o[8] = q[r][2], o[12] = q[r][3];
-      }
-      to_state(q[r][0], q[r][1], q[r][2], q[r][3], m1, km, E[r]);
-    }
-    h2_mark(a, w, it, 1);
-    if (kMode != 1) {
-    // IFFT, D = 1 .. m/2
-    layer<LA, true, 0, OM>(E, cx);
-    layer<LA, true, 1, OM>(E, cx);
-    swap_lane45(E);
-    layer<LB, true, 2, OM>(E, cx);
-    layer<LB, true, 3, OM>(E, cx);
-    swap_lane3(E, cx.lm[1]);
-    swap_lane2(E, cx.lm[0]);
-    layer<LC, true, 4, OM>(E, cx);
-    layer<LC, true, 5, OM>(E, cx);
-    exchange2(E, xb, w, lane);
-    layer<LD, true, 6, OM>(E, cx);
-    layer<LD, true, 7, OM>(E, cx);
-    exchange1(E, xb, w, lane);
-    layer<LE, true, 8, OM>(E, cx);
-    // FFT, D = m/2 .. 1
-    layer<LE, false, 8, OM>(E, cx);
-    exchange1(E, xb, w, lane);
-    layer<LD, false, 7, OM>(E, cx);
-    layer<LD, false, 6, OM>(E, cx);
-    exchange2(E, xb, w, lane);
-    layer<LC, false, 5, OM>(E, cx);
-    layer<LC, false, 4, OM>(E, cx);
-    swap_lane2(E, cx.lm[0]);
-    swap_lane3(E, cx.lm[1]);
-    layer<LB, false, 3, OM>(E, cx);
-    layer<LB, false, 2, OM>(E, cx);
-    swap_lane45(E);
-    layer<LA, false, 1, OM>(E, cx);
-    layer<LA, false, 0, OM>(E, cx);
-    }
-    h2_mark(a, w, it, 2);
-    if (kMode == 3) continue;
-    const SliceMasks ko = slice_masks();
-#pragma unroll
-    for (int r = 0; r < 4; r++) {  // parity shard s = point s
-      uint4 q0, q1, q2, q3;
-      from_state(E[r], m1, ko, q0, q1, q2, q3);
-      uint4* o = reinterpret_cast<uint4*>(dst + (pl + pos_r(LA, r)) * a.dst_sh);
-      o[0] = q0, o[4] = q1, o[8] = q2, o[12] = q3;
-    }
-    h2_mark(a, w, it, 3);
-  }
-  // the last workgroup out leaves the counters zero for the next launch on this stream
-  if (CDA_RS16_H2_SPLIT == 0 && threadIdx.x == 0 && atomicAdd(&a.queue[8], 1) == G - 1) {
-    __threadfence();
-#pragma unroll
-    for (int i = 0; i < 9; i++) __hip_atomic_store(&a.queue[i], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__global__ void __launch_bounds__(512, 2) rs_encode16_h2_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 KiB: the larger exchange (32 keys x 2 KiB)
-  __shared__ int s_item;
-  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: body<0>(a, xb, &s_item); break;
-    case 1: body<1>(a, xb, &s_item); break;
-    case 2: body<2>(a, xb, &s_item); break;
-    case 3: body<3>(a, xb, &s_item); break;
-    case 4: body<4>(a, xb, &s_item); break;
-    case 5: body<5>(a, xb, &s_item); break;
-    case 6: body<6>(a, xb, &s_item); break;
-    default: body<7>(a, xb, &s_item); break;
-  }
-}
-
-}  // namespace h2
-
 }  // namespace r16
 
 const char* rs16_diag_tag() {
@@ -1265,34 +878,9 @@ int rs16_reg_init(int device) {
     if (want != kCpoly16[i]) return -1;
   }
   return hipFuncSetAttribute((const void*)r16::rs_encode16_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             128 * 1024) == hipSuccess &&
-                 hipFuncSetAttribute((const void*)r16::h2::rs_encode16_h2_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess
+                             128 * 1024) == hipSuccess
              ? 0
              : -1;
-}
-
-#ifndef CDA_RS16_H2
-#define CDA_RS16_H2 0  // 1: the half-slice kernel (A/B builds; measured slower)
-#endif
-
-// The half-slice kernel's item counters, one set per (device, stream): launches on one stream run in order and the
-// kernel's last workgroup zeroes them, so they are zero at every launch; launches on other streams have their own.
-static int* h2_queue(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, int*> m;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  int*& p = m[{dev, s}];
-  if (!p) {
-    if (hipMalloc((void**)&p, 16 * sizeof(int)) != hipSuccess) return p = nullptr;
-    if (hipMemsetAsync(p, 0, 16 * sizeof(int), s) != hipSuccess) {
-      (void)hipFree(p);
-      return p = nullptr;
-    }
-  }
-  return p;
 }
 
 int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t s) {
@@ -1311,31 +899,18 @@ int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t 
   a.cpy_cw = j.cpy_cw;
   a.cpy_sh = j.cpy_sh;
   a.cpoly = d_cpoly;
-  a.trace = nullptr;
-  a.queue = nullptr;
-#if CDA_RS16_H2_TRACE
-  if (const char* e = getenv("CDA_H2_TRACE_PTR")) a.trace = (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0);
-  if (!a.trace) return -2;
-#endif
   a.cw_per_blk = j.cw_per_blk;
-  const bool half = CDA_RS16_H2 != 0;  // items = 256-B halves of each 512-B slice, two workgroups per CU
-  a.slices = j.shard_len / (half ? 256 : 512);
+  a.slices = j.shard_len / 512;
   const long long total = (long long)j.nblk * j.cw_per_blk * a.slices;
   if (total <= 0 || total > 0x7FFFFFFF) return -2;
   a.total = (int)total;
-  static const int ncu = [] {  // persistent workgroups: one (whole codeword) or two (half slices) per CU
+  static const int ncu = [] {  // one persistent workgroup per CU
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                  hipSuccess || n <= 0)
       n = 256;
     return n;
   }();
-  if (half) {
-    if (!(a.queue = h2_queue(s))) return -1;
-    const int grid = (int)(total < 2 * ncu ? total : 2 * ncu);
-    hipLaunchKernelGGL(r16::h2::rs_encode16_h2_kernel, dim3((unsigned)grid), dim3(512), 64 * 1024, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
   const int grid = (int)(total < ncu ? total : ncu);
   hipLaunchKernelGGL(r16::rs_encode16_reg_kernel, dim3((unsigned)grid), dim3(1024), 128 * 1024, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
