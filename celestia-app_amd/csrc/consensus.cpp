@@ -281,7 +281,10 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // Input: pageable hipMemcpyAsync (the runtime pins the caller's written pages on the fly).  Roots only: one copy,
 // 0.467 ms per block, against 0.553 ms in four bands (each pageable copy pays its own set-up) and 0.59 ms staged
 // through a pinned slab by the copy pool (profiles/r04_pass2.log).  With the EDS: four bands, so that the first
-// band's Q1 goes down while the rest comes up (reused output 0.73 vs 0.76-0.78 ms, r04_pass5.log).
+// band's Q1 goes down while the rest comes up (reused output 0.73 vs 0.76-0.78 ms, r04_pass5.log).  Pinning the
+// caller's shares for the call (hipHostRegister: an asynchronous H2D with the kernels queued behind it at once) gave
+// 0.447 vs 0.452 ms roots only and was slower with the EDS (r04_pass8.log): the rows pass of one block is
+// latency-bound (~20 us whatever its size), so the device chain after the input is the same either way.
 // Output, by what the caller's EDS buffer is:
 //   pinned      Q1 and the bottom half straight to it by DMA;
 //   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
