@@ -133,7 +133,8 @@ def _batchable(blobs):
 
 def precompute_commitments(txs, subtree_root_threshold=appconsts.SUBTREE_ROOT_THRESHOLD, ctx=None):
     """The pre-pass: every BlobTx's commitments in ONE cda_blob_commitments call.  -> list (one entry per tx): the
-    tx's commitments, or None for a normal tx / a BlobTx with a blob ValidateBlobs would reject."""
+    tx's commitments, or None for a normal tx / a BlobTx with a blob ValidateBlobs would reject / every tx when the
+    batch call fails (go/patches/0003 PrecomputeCommitments: the per-tx checks then compute their own)."""
     parsed = [unmarshal_blob_tx(t) for t in txs]
     take = [i for i, p in enumerate(parsed) if p is not None and _batchable(p[1])]
     out = [None] * len(txs)
@@ -141,8 +142,13 @@ def precompute_commitments(txs, subtree_root_threshold=appconsts.SUBTREE_ROOT_TH
         return out
     blobs = [b for i in take for b in parsed[i][1]]
     ctx = ctx or N.default_context()
-    got = ctx.blob_commitments([b["ns"] for b in blobs], [b["data"] for b in blobs],
-                               [b["share_version"] for b in blobs], subtree_root_threshold)
+    try:
+        got = ctx.blob_commitments([b["ns"] for b in blobs], [b["data"] for b in blobs],
+                                   [b["share_version"] for b in blobs], subtree_root_threshold)
+    except N.CdaError:
+        return out  # as the Go pre-pass: a failed batch leaves every tx to compute its own commitments
+    if len(got) != len(blobs):
+        return out
     pos = 0
     for i in take:
         n = len(parsed[i][1])

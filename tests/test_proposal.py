@@ -140,6 +140,27 @@ def test_first_invalid_blob_tx_is_reported(which):
     assert eng.calls <= 2  # the batch (+ one per-tx call only for a tx left out of the batch)
 
 
+class FailingBatch(OracleCommitments):
+    """The batch call fails (a device error); per-tx calls succeed."""
+
+    def blob_commitments(self, namespaces, datas, share_versions=None, subtree_root_threshold=64):
+        if self.calls == 0:
+            self.calls += 1
+            from cda import _native as N
+            raise N.CdaError(-5, "injected batch failure")
+        return super().blob_commitments(namespaces, datas, share_versions, subtree_root_threshold)
+
+
+def test_failed_batch_falls_back_to_per_tx():
+    txs = random_proposal(11)
+    eng = FailingBatch()
+    assert P.precompute_commitments(txs, ctx=eng) == [None] * len(txs)
+    eng = FailingBatch()
+    assert P.process_proposal_blob_txs(txs, ctx=eng) == (None, None)
+    n_blob_txs = sum(S.unmarshal_blob_tx(t) is not None for t in txs)
+    assert eng.calls == 1 + n_blob_txs
+
+
 def test_batched_and_per_tx_agree():
     txs = random_proposal(5)
     eng = OracleCommitments()
