@@ -392,7 +392,26 @@ struct Args {
   long long cpy_blk, cpy_cw, cpy_sh;
   const uint16_t* cpoly;
   int cw_per_blk, slices, total;  // total = codewords of the launch
+#if CDA_RS16_TRACE
+  unsigned long long* trace;  // diagnostic builds: s_memrealtime at 4 points of the first 8 codewords of each workgroup
+#endif
 };
+
+#ifndef CDA_RS16_TRACE
+#define CDA_RS16_TRACE 0
+#endif
+// trace[(blockIdx * 8 + it) * 4 + ph] by lane 0 of wave 0 (vector store); ph 0 = codeword in registers (top part
+// done), 1 = last LDS exchange done, 2 = transforms done, 3 = stores (and the next codeword's direct loads) issued
+__device__ __forceinline__ void rs16_mark(const Args& a, int w, int it, int ph) {
+#if CDA_RS16_TRACE
+  if (w == 0 && it < 8) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) a.trace[((size_t)blockIdx.x * 8 + it) * 4 + ph] = t;
+  }
+#else
+  (void)a, (void)w, (void)it, (void)ph;
+#endif
+}
 
 // Diagnostic builds only (scripts/gpu_rs16_diag.sh compiles a separate library with -DCDA_RS16_DIAG_MODE=N):
 // 1 = loads + stores only; 2 = no loads; 3 = no loads, no stores.  A release build is always 0 (encode) -- no
@@ -756,7 +775,8 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
   }
   uint32_t E[4][16];
   top_part<OM, 8>(a, xw, w, g, cx, R, E);  // after the prologue only its 8 R loads follow the prefetch
-  for (;;) {
+  for (int it = 0;; it++) {
+    rs16_mark(a, w, it, 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) asm volatile("" : "+v"(cx.lv[i]));
     asm volatile("" : "+v"(cx.lm3));
@@ -792,6 +812,7 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
     layer<LD, false, 6, OM>(E, cx);
     layer<LD, false, 5, OM>(E, cx);
     exchange_w<0>(E, xb, w, lane);  // ends with a barrier: the exchange buffer is free until the next codeword
+    rs16_mark(a, w, it, 1);
     prefetch01(srcn, shn, pl, xw);
     layer<LC, false, 4, OM>(E, cx);
     layer<LC, false, 3, OM>(E, cx);
@@ -800,6 +821,7 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
     swap_lane45(E);
     layer<LA, false, 1, OM>(E, cx);
     layer<LA, false, 0, OM>(E, cx);
+    rs16_mark(a, w, it, 2);
     {  // parity shard s = point s; r = 2, 3 first, each followed by the next codeword's loads of that position
       uint32_t m1 = (lane & 2) ? ~0u : 0u;
       asm volatile("" : "+v"(m1));
@@ -820,6 +842,7 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
         }
       }
     }
+    rs16_mark(a, w, it, 3);
     if (!more) break;
     g = gn;
     top_part<OM, kAfterPrefetch>(a, xw, w, g, cx, R, E);
@@ -900,6 +923,11 @@ int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t 
   a.cpy_sh = j.cpy_sh;
   a.cpoly = d_cpoly;
   a.cw_per_blk = j.cw_per_blk;
+#if CDA_RS16_TRACE
+  a.trace = nullptr;
+  if (const char* e = getenv("CDA_RS16_TRACE_PTR")) a.trace = (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0);
+  if (!a.trace) return -2;
+#endif
   a.slices = j.shard_len / 512;
   const long long total = (long long)j.nblk * j.cw_per_blk * a.slices;
   if (total <= 0 || total > 0x7FFFFFFF) return -2;
