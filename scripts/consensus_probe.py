@@ -51,6 +51,38 @@ res["fresh_with_eds"] = series(True, True)
 res["fresh_roots_only"] = series(False, True)
 res["reused_with_eds"] = series(True, False)
 res["reused_roots_only"] = series(False, False)
+
+
+def pinned_series():
+    """A caller that keeps pinned buffers (cda_host_alloc) for the shares and the EDS: both DMAs direct."""
+    pb_ods, pb_eds = ctx.pinned((1, k * k, 512)), ctx.pinned((1, w * w, 512))
+    pin_ods, pin_eds = pb_ods.array, pb_eds.array
+    out = []
+    for i in range(reps + 2):
+        pin_ods[0] = ods
+        t0 = time.perf_counter()
+        _, _, _, dah = ctx.extend_commit_batch(pin_ods, eds_out=pin_eds)
+        el = (time.perf_counter() - t0) * 1e3
+        if bytes(dah[0]) != dah_ref:
+            raise RuntimeError("DAH mismatch")
+        if i >= 2:
+            out.append(el)
+    if not np.array_equal(pin_eds.reshape(eds_ref.shape), eds_ref):
+        raise RuntimeError("EDS mismatch")
+    pb_ods.free()
+    pb_eds.free()
+    return {"min": round(min(out), 3), "median": round(float(np.median(out)), 3), "max": round(max(out), 3)}
+
+
+res["pinned_with_eds"] = pinned_series()
+try:  # where the process runs relative to the GPU (host placement moves the D2H rate between boxes)
+    pr = torch.cuda.get_device_properties(0)
+    bdf = "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+    res["gpu_numa_node"] = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+except Exception as e:  # noqa: BLE001
+    res["gpu_numa_node"] = repr(e)[:80]
+cpus = sorted(os.sched_getaffinity(0))
+res["cpus"] = f"{len(cpus)}: {cpus[0]}-{cpus[-1]}" if cpus else "none"
 print(json.dumps(res), flush=True)
 if os.environ.get("CDA_CONSENSUS", "1") != "0" and os.environ.get("CDA_PROBE_SWEEP"):  # copy-pool size sweep (a context reads CDA_COPY_THREADS at its first call)
     sweep = {}
