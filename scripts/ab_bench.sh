@@ -11,7 +11,7 @@ mkdir -p gpurun_out
 for i in $(seq 0 $((N - 1))); do
   for j in $(seq 0 $((M - 1))); do
     lib=${LIBS[$(((i + j) % M))]}
-    CDA_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > gpurun_out/ab_run.log 2>&1 || exit 1
+    CDA_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-k512-split > gpurun_out/ab_run.log 2>&1 || exit 1
     python3 -c "
 import json
 for l in open('gpurun_out/ab_run.log'):
