@@ -132,7 +132,7 @@ struct Consensus {
   uint8_t* d_res = nullptr;    // the same on the device: one D2H of the results
   size_t cap_out = 0, cap_res = 0, cap_dres = 0;
   hipEvent_t ev_in[kMaxBands] = {}, ev_rows[kMaxBands] = {}, ev_q1[kMaxBands] = {}, ev_cols = nullptr,
-             ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr;
+             ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr, ev_stg[kMaxPieces] = {};
   ~Consensus() {
     delete pool;
     for (uint8_t* p : {pin_out, pin_res})
@@ -142,6 +142,8 @@ struct Consensus {
       for (hipEvent_t e : {ev_in[i], ev_rows[i], ev_q1[i]})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_cols, ev_done, ev_h2d_end, ev_d2h_end})
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_stg)
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -197,6 +199,8 @@ int get_consensus(cda_ctx* c, Consensus*& out) {
          hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->ev_h2d_end, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->ev_d2h_end, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < Consensus::kMaxPieces && ok; i++)
+      ok = hipEventCreateWithFlags(&s->ev_stg[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
       delete s;
       c->last_err = "consensus path: event creation failed";
@@ -324,7 +328,17 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
   const bool banded = in_mode_env ? in_mode_env == 1 : want;
-  if ((want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b))) ||
+  // A pageable output's bottom half comes down in two concurrent halves: the front by pageable DMA on the D2H
+  // stream, the back through the pinned slab on the second stream, copied out by the pool chunk by chunk as it lands.
+  // The pageable DMA alone ran at 36-46 GB/s; side by side the two fill the link (fresh output 0.75-0.79 vs
+  // 0.89-0.92 ms, written 0.73-0.77 vs 0.75-0.80; staging 4 / 10 / 12 of the 16 MiB was slower, r04_pass12/13.log).
+  // CDA_CONS_STG = MiB to stage instead (0: all pageable; A/B runs).
+  const char* e_stg = getenv("CDA_CONS_STG");
+  const size_t stg_want = e_stg ? ((size_t)std::max(0, atoi(e_stg)) << 20) : bot_b / 2;
+  const size_t stg_b = (want && !out_pinned) ? std::min(bot_b / 4 * 3, stg_want / (2 * erowS) * (2 * erowS)) : 0;
+  const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
+  const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
+  if ((want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
       (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
     return rc;
   if (fresh) want_huge_pages(eds_or_null, eds_b);
@@ -340,7 +354,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const int n_touch = fresh ? (int)std::max<size_t>(1, bot_b >> 21) : 0;
   const int n_piece = fresh ? std::min(Consensus::kMaxPieces, std::max(1, n_touch / 2)) : 1;
   std::atomic<bool> abort{false};
-  std::atomic<int> q1_rec{0};
+  std::atomic<int> q1_rec{0}, stg_rec{0};
   std::atomic<int> touched[Consensus::kMaxPieces];
   for (int p = 0; p < Consensus::kMaxPieces; p++) touched[p].store(0);
 
@@ -377,6 +391,16 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
             for (uint32_t r = r0; r < std::min((b + 1) * kb, r0 + rows_per_task); r++)
               memcpy(eds_or_null + r * erowS + rowS, X->pin_out + r * rowS, rowS);
           });
+    for (int j = 0; j < n_stg; j++) {  // staged chunk j of the bottom half's tail, four copy tasks each
+      const size_t lo = stg_b * j / n_stg, hi = stg_b * (j + 1) / n_stg;
+      for (int h = 0; h < 4; h++) {
+        const size_t a0 = lo + (hi - lo) * h / 4, a1 = lo + (hi - lo) * (h + 1) / 4;
+        tasks.emplace_back([=, &stg_rec, &abort] {
+          if (!wait_count(stg_rec, j + 1, abort) || !wait_event(X->ev_stg[j], abort)) return;
+          memcpy(eds_or_null + k * erowS + dir_b + a0, X->pin_out + q1_b + a0, a1 - a0);
+        });
+      }
+    }
   }
   X->pool->start(&tasks);
   mark(1);
@@ -433,6 +457,17 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
           hipSuccess)
     fail = "bottom D2H";
+  if (!fail && n_stg && hipStreamWaitEvent(c->h2d_stream, X->ev_cols, 0) != hipSuccess) fail = "event";
+  for (int j = 0; j < n_stg && !fail; j++) {
+    const size_t lo = stg_b * j / n_stg, hi = stg_b * (j + 1) / n_stg;
+    if (hipMemcpyAsync(X->pin_out + q1_b + lo, d_eds + k * erowS + dir_b + lo, hi - lo, hipMemcpyDeviceToHost,
+                       c->h2d_stream) != hipSuccess ||
+        hipEventRecord(X->ev_stg[j], c->h2d_stream) != hipSuccess) {
+      fail = "staged D2H";
+      break;
+    }
+    stg_rec.store(j + 1, std::memory_order_release);
+  }
   if (!fail) {
     if ((rc = enqueue_commit(c, k, 1, d_eds, d_roots, d_dah, d_status, s, 0, false))) {
       frc = rc;
@@ -452,9 +487,9 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       while (touched[p].load(std::memory_order_acquire) < need && !abort.load(std::memory_order_relaxed))
         std::this_thread::yield();
     }
-    const size_t lo = bot_b * p / n_piece, hi = bot_b * (p + 1) / n_piece;
-    if (hipMemcpyAsync(eds_or_null + k * erowS + lo, d_eds + k * erowS + lo, hi - lo, hipMemcpyDeviceToHost,
-                       c->d2h_stream) != hipSuccess)
+    const size_t lo = std::min(dir_b, bot_b * p / n_piece), hi = std::min(dir_b, bot_b * (p + 1) / n_piece);
+    if (hi > lo && hipMemcpyAsync(eds_or_null + k * erowS + lo, d_eds + k * erowS + lo, hi - lo,
+                                  hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess)
       fail = "bottom D2H";
   }
   if (!fail && (hipEventRecord(X->ev_h2d_end, c->h2d_stream) != hipSuccess ||

@@ -51,14 +51,18 @@ def test_one_block_fresh_buffers(ctx, k, want_eds):
 
 
 @pytest.mark.parametrize("cons_in,cons_out", [("1", "0"), ("2", "0"), ("1", "2"), ("2", "2")])
+@pytest.mark.parametrize("stg", [None, "0", "3"])
 @pytest.mark.parametrize("k", [16, 128])
 @pytest.mark.parametrize("buf", ["fresh", "written"])
-def test_one_block_forms(ctx, monkeypatch, cons_in, cons_out, k, buf):
+def test_one_block_forms(ctx, monkeypatch, cons_in, cons_out, stg, k, buf):
     """Every input form (CDA_CONS_IN: four bands / one copy) with every pageable output form (CDA_CONS_OUT=0: chosen
     by residency -- fresh buffers are touched by the pool and sent in pieces; 2: the written-buffer form forced, so
-    the runtime faults a fresh buffer in itself), fresh and written output buffers."""
+    the runtime faults a fresh buffer in itself) and bottom-half split (CDA_CONS_STG: default half staged through the
+    pinned slab, 0 = all pageable, 3 MiB), fresh and written output buffers."""
     monkeypatch.setenv("CDA_CONS_IN", cons_in)
     monkeypatch.setenv("CDA_CONS_OUT", cons_out)
+    if stg is not None:
+        monkeypatch.setenv("CDA_CONS_STG", stg)
     ods = O.gen_ods(k, 0xF0F0 + k)
     out = np.empty((1, 4 * k * k, 512), np.uint8) if buf == "fresh" else np.full((1, 4 * k * k, 512), 0x3C, np.uint8)
     eds, rr, cr, dah = ctx.extend_commit_batch(ods[None].copy(), eds_out=out)
