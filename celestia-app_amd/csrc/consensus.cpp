@@ -328,13 +328,14 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
   const bool banded = in_mode_env ? in_mode_env == 1 : want;
-  // A pageable output's bottom half comes down in two concurrent halves: the front by pageable DMA on the D2H
-  // stream, the back through the pinned slab on the second stream, copied out by the pool chunk by chunk as it lands.
-  // The pageable DMA alone ran at 36-46 GB/s; side by side the two fill the link (fresh output 0.75-0.79 vs
-  // 0.89-0.92 ms, written 0.73-0.77 vs 0.75-0.80; staging 4 / 10 / 12 of the 16 MiB was slower, r04_pass12/13.log).
-  // CDA_CONS_STG = MiB to stage instead (0: all pageable; A/B runs).
+  // A pageable output's bottom half comes down in two concurrent parts: the front by pageable DMA on the D2H stream,
+  // the back through the pinned slab on the second stream, copied out by the pool chunk by chunk as it lands.  The
+  // pageable DMA alone ran at 36-46 GB/s; side by side the two fill the link.  Staged share, same box
+  // (r04_pass12..14.log, k = 128, 16 MiB bottom half): fresh output 0 / 6 / 8 / 10 / 12 MiB -> 0.86 / 0.77 / 0.755
+  // / 0.84 / 0.86-0.97 ms, written output 0 / 6 / 8 MiB -> 0.73 / 0.71 / 0.77 ms; so half for a fresh buffer,
+  // 3/8 for a written one.  CDA_CONS_STG = MiB to stage instead (0: all pageable; A/B runs).
   const char* e_stg = getenv("CDA_CONS_STG");
-  const size_t stg_want = e_stg ? ((size_t)std::max(0, atoi(e_stg)) << 20) : bot_b / 2;
+  const size_t stg_want = e_stg ? ((size_t)std::max(0, atoi(e_stg)) << 20) : (fresh ? bot_b / 2 : bot_b / 8 * 3);
   const size_t stg_b = (want && !out_pinned) ? std::min(bot_b / 4 * 3, stg_want / (2 * erowS) * (2 * erowS)) : 0;
   const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
   const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
