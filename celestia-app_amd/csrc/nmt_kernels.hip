@@ -354,6 +354,23 @@ __global__ void __launch_bounds__(256) dah_wide_kernel(const uint4* __restrict__
 // put back to 0 for the next call) folds the block's digests into the DAH, so the step needs no DAH launch.  The
 // batched form (nmt_levels_kernel + dah_kernel) keeps every lane on a useful node and stays the throughput path.
 constexpr int kLdsRec = 7;  // uint4 per LDS record
+#ifndef CDA_TREES_TRACE
+#define CDA_TREES_TRACE 0  // diagnostic builds: per-workgroup phase timestamps of trees_lds_kernel
+#endif
+#if CDA_TREES_TRACE
+__device__ unsigned long long* g_trees_trace;  // [workgroup][16 slots][realtime, shader clock]
+#endif
+__device__ __forceinline__ void trees_mark(int slot) {
+#if CDA_TREES_TRACE
+  if (threadIdx.x == 0 && g_trees_trace) {
+    const unsigned long long rt = __builtin_amdgcn_s_memrealtime(), ck = __builtin_amdgcn_s_memtime();
+    g_trees_trace[((size_t)blockIdx.x * 16 + slot) * 2] = rt;
+    g_trees_trace[((size_t)blockIdx.x * 16 + slot) * 2 + 1] = ck;
+  }
+#else
+  (void)slot;
+#endif
+}
 __device__ __forceinline__ void load_pair(const uint4* in, int i, uint32_t (&L)[24], uint32_t (&R)[24]) {
 #pragma unroll
   for (int q = 0; q < 6; q++) {
@@ -374,6 +391,7 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   const bool col = tree >= (unsigned)w;
   const unsigned t = tree & (w - 1);
   const uint4* lb = leaves + (size_t)b * w * w * 6;
+  trees_mark(0);
   if (threadIdx.x == 0) last = 0;  // published by the barrier after the leaf copy
   uint4* A = lds + (size_t)half * (w + w / 2) * kLdsRec;
   uint4* B = A + (size_t)w * kLdsRec;
@@ -385,6 +403,7 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
     A[i * kLdsRec + q] = lb[rec * 6 + q];
   }
   __syncthreads();
+  trees_mark(1);
   for (int l = 1; l <= log2w; l++) {
     const uint4* in = (l & 1) ? A : B;
     uint4* out = (l & 1) ? B : A;
@@ -426,6 +445,7 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
       }
     }
     __syncthreads();
+    trees_mark(1 + l);
   }
   const uint4* root = (log2w & 1) ? B : A;
   uint4* rout = roots + ((size_t)b * n + tree) * 6;
@@ -456,18 +476,22 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
     }
   }
   __syncthreads();  // both halves' roots and digests are stored (each by lanes of the wave that increments below)
+  trees_mark(11);
   if (threadIdx.x == 0 || threadIdx.x == 128) {  // one increment per tree, from the wave that stored it
     const unsigned prev = __hip_atomic_fetch_add(done + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (unsigned)n - 1) last = 1;  // at most one tree of a block is its last
   }
   __syncthreads();
+  trees_mark(12);
   if (!last) return;
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the other workgroups' digests (released before their increments)
   uint32_t* sdig = reinterpret_cast<uint32_t*>(lds);
   const uint4* src = reinterpret_cast<const uint4*>(digests + (size_t)b * n * 8);
   for (int x = threadIdx.x; x < n * 2; x += blockDim.x) reinterpret_cast<uint4*>(sdig)[x] = src[x];
   __syncthreads();
+  trees_mark(13);
   dah_fold_kw(sdig, n, dah + b * 8, sdig + (n + (n + 1) / 2) * 8);
+  trees_mark(14);
   if (threadIdx.x == 0) __hip_atomic_store(done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -592,6 +616,14 @@ int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned*
       hipFuncSetAttribute((const void*)trees_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
           hipSuccess)
     return -1;
+#if CDA_TREES_TRACE
+  {
+    unsigned long long* tp = nullptr;
+    if (const char* e = getenv("CDA_TREES_TRACE_PTR")) tp = (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0);
+    if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_trees_trace), &tp, sizeof tp, 0, hipMemcpyHostToDevice, s) != hipSuccess)
+      return -1;
+  }
+#endif
   hipLaunchKernelGGL(trees_lds_kernel, dim3((unsigned)nblocks * w), dim3(256), lds, s,
                      (const uint4*)d_leaves, (uint4*)d_roots, (uint32_t*)d_dah, d_done, (uint32_t*)d_digests, log2w);
   return hipGetLastError() == hipSuccess ? 0 : -1;
