@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out
 true && touch gpurun_out/r04l_tests.log
 rc=$?; tail -n 2 gpurun_out/r04l_tests.log; [ $rc -ne 0 ] && exit $rc
-for v in "CDA_CONS_TRACE=" "CDA_PROBE_SWEEP=1" "CDA_PROBE_SWEEP=1"; do
+for v in "CDA_CONS_H2D2=0" "CDA_CONS_H2D2=1" "CDA_CONS_H2D2=0" "CDA_CONS_H2D2=1" "CDA_CONS_H2D2=0"; do
   env -u CDA_CONS_TRACE $v timeout -k 10 300 python -u scripts/consensus_probe.py 20 > gpurun_out/r04l_probe.log 2>&1
   rc=$?; echo "== $v $(grep '^{' gpurun_out/r04l_probe.log)"; [ $rc -ne 0 ] && { tail -5 gpurun_out/r04l_probe.log; exit $rc; }
 done
