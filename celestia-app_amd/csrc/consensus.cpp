@@ -291,11 +291,11 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // latency-bound (~20 us whatever its size), so the device chain after the input is the same either way.
 // Output, by what the caller's EDS buffer is:
 //   pinned      Q1 and the bottom half straight to it by DMA;
-//   resident    Q1 through the pinned slab (copy pool), the bottom half by one pageable DMA, which pins the written
-//               pages cheaply and runs near the link rate;
+//   resident    Q1 through the pinned slab (copy pool), the bottom half split between a pageable DMA (the written
+//               pages pin cheaply) and the pinned slab (below);
 //   fresh       huge pages asked for and every page first touched by the pool (one 2 MiB range per task) while the
-//               device works, then the resident form with the bottom half in four pieces, each sent once its pages
-//               are touched.  A pageable DMA into never-touched memory faults it page by page in one thread (3.6 ms
+//               device works, then the resident form, the pageable part of the bottom half in pieces, each sent once
+//               its pages are touched.  A pageable DMA into never-touched memory faults it page by page in one thread (3.6 ms
 //               per block, r04_pass1); sending the bottom half through the pinned slab in 1 MiB chunks copied out by
 //               the pool took 1.02-1.23 ms against 0.80-0.88 ms for this form (r04_pass4.log); registering it
 //               (hipHostRegister, async DMA, unregister) was no faster.
