@@ -177,7 +177,7 @@ __device__ __forceinline__ void ld4(const uint4* p, uint32_t* w) {  // 4 x 16 B 
 // reads are neither merged nor hoisted and kept live, and each compression is
 // fenced: 89 VGPRs (5 waves/SIMD) instead of 205 when both children stayed in
 // registers.
-__device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po) {
+__device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po, bool store = true) {
   uint32_t st[8], m[16];
   sha256_init(st);
   // message = 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits); 48 words
@@ -241,8 +241,9 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
   for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
   o[22] = d[7] >> 16;
   o[23] = 0;
+  if (store)
 #pragma unroll
-  for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+    for (int i = 0; i < 6; i++) po[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
 }
 
 // Message block B (0..2) of an inner node: 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits), children in

@@ -258,30 +258,31 @@ __device__ __forceinline__ void dah_fold_kw(uint32_t* sdig, int n, uint32_t* out
         for (int t = 0; t < 8; t++) o[t] = st[t];
       }
     } else {
+      // every lane of waves 0 and 1 computes, with full exec masks (lanes past the level's pairs hash stale,
+      // in-bounds LDS words and store nothing), as in trees_lds_kernel
       const int i = threadIdx.x & 63;
       const bool pair = i < out_cnt && 2 * i + 1 < cnt;
       uint32_t st[8];
-      if (threadIdx.x < 64 && i < out_cnt) {
+      if (threadIdx.x < 64) {
         const uint32_t* Ld = src + (2 * i) * 8;
-        if (pair) {
-          uint32_t m[16];
-          sha256_init(st);
-          rfc_node_block<0>(Ld, src + (2 * i + 1) * 8, m);
-          sha256_compress(st, m);
-        } else {
+        if (i < out_cnt && !pair)
 #pragma unroll
           for (int t = 0; t < 8; t++) dst[i * 8 + t] = Ld[t];
-        }
-      } else if (threadIdx.x >= 64 && threadIdx.x < 128 && pair) {
+        uint32_t m[16];
+        sha256_init(st);
+        rfc_node_block<0>(Ld, src + (2 * i + 1) * 8, m);
+        sha256_compress(st, m);
+      } else if (threadIdx.x < 128) {
         uint32_t m[16];
         rfc_node_block<1>(src + (2 * i) * 8, src + (2 * i + 1) * 8, m);
         sha256_kw_store(m, kw + i * kKwStride);
       }
       __syncthreads();
-      if (threadIdx.x < 64 && pair) {
+      if (threadIdx.x < 64) {
         sha256_rounds_kw(st, kw + i * kKwStride);
+        if (pair)
 #pragma unroll
-        for (int t = 0; t < 8; t++) dst[i * 8 + t] = st[t];
+          for (int t = 0; t < 8; t++) dst[i * 8 + t] = st[t];
       }
     }
     __syncthreads();
@@ -358,17 +359,31 @@ constexpr int kLdsRec = 7;  // uint4 per LDS record
 #define CDA_TREES_TRACE 0  // diagnostic builds: per-workgroup phase timestamps of trees_lds_kernel
 #endif
 #if CDA_TREES_TRACE
-__device__ unsigned long long* g_trees_trace;  // [workgroup][16 slots][realtime, shader clock]
+__device__ unsigned long long* g_trees_trace;  // [workgroup][32 slots][realtime, shader clock]
 #endif
-__device__ __forceinline__ void trees_mark(int slot) {
+// the stamps go to LDS (thread 0) and to memory at the end, so no global store sits between the phases
+struct TreesStamps {
+  unsigned long long* v;  // LDS: [32][rt, clock]
+};
+__device__ __forceinline__ void trees_mark(TreesStamps& ts, int slot) {
 #if CDA_TREES_TRACE
-  if (threadIdx.x == 0 && g_trees_trace) {
-    const unsigned long long rt = __builtin_amdgcn_s_memrealtime(), ck = __builtin_amdgcn_s_memtime();
-    g_trees_trace[((size_t)blockIdx.x * 16 + slot) * 2] = rt;
-    g_trees_trace[((size_t)blockIdx.x * 16 + slot) * 2 + 1] = ck;
+  if (threadIdx.x == 0) {
+    ts.v[2 * slot] = __builtin_amdgcn_s_memrealtime();
+    ts.v[2 * slot + 1] = __builtin_amdgcn_s_memtime();
   }
 #else
-  (void)slot;
+  (void)ts, (void)slot;
+#endif
+}
+__device__ __forceinline__ void trees_flush(const TreesStamps& ts, int lo, int hi) {
+#if CDA_TREES_TRACE
+  if (threadIdx.x == 0 && g_trees_trace)
+    for (int s = lo; s < hi; s++) {
+      g_trees_trace[((size_t)blockIdx.x * 32 + s) * 2] = ts.v[2 * s];
+      g_trees_trace[((size_t)blockIdx.x * 32 + s) * 2 + 1] = ts.v[2 * s + 1];
+    }
+#else
+  (void)ts, (void)lo, (void)hi;
 #endif
 }
 __device__ __forceinline__ void load_pair(const uint4* in, int i, uint32_t (&L)[24], uint32_t (&R)[24]) {
@@ -391,7 +406,13 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
   const bool col = tree >= (unsigned)w;
   const unsigned t = tree & (w - 1);
   const uint4* lb = leaves + (size_t)b * w * w * 6;
-  trees_mark(0);
+#if CDA_TREES_TRACE
+  __shared__ unsigned long long tstamp[64];
+  TreesStamps tst{tstamp};
+#else
+  TreesStamps tst{nullptr};
+#endif
+  trees_mark(tst, 0);
   if (threadIdx.x == 0) last = 0;  // published by the barrier after the leaf copy
   uint4* A = lds + (size_t)half * (w + w / 2) * kLdsRec;
   uint4* B = A + (size_t)w * kLdsRec;
@@ -403,7 +424,7 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
     A[i * kLdsRec + q] = lb[rec * 6 + q];
   }
   __syncthreads();
-  trees_mark(1);
+  trees_mark(tst, 1);
   for (int l = 1; l <= log2w; l++) {
     const uint4* in = (l & 1) ? A : B;
     uint4* out = (l & 1) ? B : A;
@@ -418,16 +439,19 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
       }
     } else {
       // wave 0 of the half hashes block 0 of node ht while wave 1 expands blocks 1 and 2 of node ht - 64; after
-      // the barrier wave 0 runs the last two compressions from the precomputed schedules
+      // the barrier wave 0 runs the last two compressions from the precomputed schedules.  Every lane computes, also
+      // past the level's last node (on stale, in-bounds records; only lanes < nodes write): with the waves' exec
+      // masks partly off, levels of <= 16 nodes took 9.4-10.8 us instead of 6.8 (r04_trees_trace.log)
       const int i = ht & 63;
       uint32_t L[24], R[24], st[8];
-      if (i < nodes) load_pair(in, i, L, R);
-      if (ht < 64 && i < nodes) {
+      load_pair(in, i, L, R);
+      if (ht < 64) {
         uint32_t m[16];
         sha256_init(st);
         node_block<0>(L, R, m);
         sha256_compress(st, m);
-      } else if (ht >= 64 && i < nodes) {
+        trees_mark(tst, 2 + 3 * (l - 1));
+      } else {
         uint32_t m[16];
         node_block<1>(L, R, m);
         sha256_kw_store(m, kw + i * kKwStride);
@@ -435,63 +459,68 @@ __global__ void __launch_bounds__(256) trees_lds_kernel(const uint4* __restrict_
         sha256_kw_store(m, kw + (64 + i) * kKwStride);
       }
       __syncthreads();
-      if (ht < 64 && i < nodes) {
+      trees_mark(tst, 3 + 3 * (l - 1));
+      if (ht < 64) {
         sha256_rounds_kw(st, kw + i * kKwStride);
         sha256_rounds_kw(st, kw + (64 + i) * kKwStride);
         uint32_t o[24];
         node_record(L, R, st, o);
+        if (i < nodes)
 #pragma unroll
-        for (int q = 0; q < 6; q++) out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+          for (int q = 0; q < 6; q++)
+            out[i * kLdsRec + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
       }
     }
     __syncthreads();
-    trees_mark(1 + l);
+    trees_mark(tst, 4 + 3 * (l - 1));
   }
   const uint4* root = (log2w & 1) ? B : A;
   uint4* rout = roots + ((size_t)b * n + tree) * 6;
   if (ht < 6) rout[ht] = root[ht];
-  {  // this root's DAH leaf digest: block 0 by lane 0, block 1's schedule by lane 64 meanwhile
+  {  // this root's DAH leaf digest: block 0 by wave 0, block 1's schedule by wave 1 meanwhile (every lane of both
+     // waves computes the same digest into its own schedule row, with full exec masks; lane 0 stores it)
     uint32_t L[24], st[8], m[16];
-    if (ht == 0 || ht == 64) {
 #pragma unroll
-      for (int q = 0; q < 6; q++) {
-        const uint4 u = root[q];
-        L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
-      }
+    for (int q = 0; q < 6; q++) {
+      const uint4 u = root[q];
+      L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
     }
-    if (ht == 0) {
+    uint32_t* kwl = kw + (ht & 63) * kKwStride;
+    if (ht < 64) {
       sha256_init(st);
       dah_leaf_block<0>(L, m);
       sha256_compress(st, m);
-    } else if (ht == 64) {
+    } else {
       dah_leaf_block<1>(L, m);
-      sha256_kw_store(m, kw);
+      sha256_kw_store(m, kwl);
     }
     __syncthreads();
+    if (ht < 64) sha256_rounds_kw(st, kwl);
     if (ht == 0) {
-      sha256_rounds_kw(st, kw);
       uint4* dg = reinterpret_cast<uint4*>(digests + ((size_t)b * n + tree) * 8);
       dg[0] = make_uint4(st[0], st[1], st[2], st[3]);
       dg[1] = make_uint4(st[4], st[5], st[6], st[7]);
     }
   }
   __syncthreads();  // both halves' roots and digests are stored (each by lanes of the wave that increments below)
-  trees_mark(11);
+  trees_mark(tst, 26);
   if (threadIdx.x == 0 || threadIdx.x == 128) {  // one increment per tree, from the wave that stored it
     const unsigned prev = __hip_atomic_fetch_add(done + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (unsigned)n - 1) last = 1;  // at most one tree of a block is its last
   }
   __syncthreads();
-  trees_mark(12);
+  trees_mark(tst, 27);
+  trees_flush(tst, 0, 28);
   if (!last) return;
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the other workgroups' digests (released before their increments)
   uint32_t* sdig = reinterpret_cast<uint32_t*>(lds);
   const uint4* src = reinterpret_cast<const uint4*>(digests + (size_t)b * n * 8);
   for (int x = threadIdx.x; x < n * 2; x += blockDim.x) reinterpret_cast<uint4*>(sdig)[x] = src[x];
   __syncthreads();
-  trees_mark(13);
+  trees_mark(tst, 28);
   dah_fold_kw(sdig, n, dah + b * 8, sdig + (n + (n + 1) / 2) * 8);
-  trees_mark(14);
+  trees_mark(tst, 29);
+  trees_flush(tst, 28, 30);
   if (threadIdx.x == 0) __hip_atomic_store(done + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -782,9 +811,19 @@ __global__ void __launch_bounds__(256) axes_verify_kernel(const uint8_t* __restr
   }
   __syncthreads();
   for (int l = 1; l <= log2w; l++) {
-    for (int i = threadIdx.x; i < (w >> l); i += blockDim.x)
+    const int nodes = w >> l;
+    if (nodes >= 64) {
+      for (int i = threadIdx.x; i < nodes; i += blockDim.x)
+        hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
+                      lnodes + ((size_t)i << l) * 6);
+    } else if (threadIdx.x < 64) {
+      // a level of < 64 nodes: the whole wave computes with a full exec mask (lanes past the last node hash node 0
+      // again and store nothing; reads precede the stores within the wave) -- partly masked waves ran the tree
+      // kernels' small levels ~40 % slower (r04_trees_trace.log)
+      const int i = (int)threadIdx.x < nodes ? (int)threadIdx.x : 0;
       hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
-                    lnodes + ((size_t)i << l) * 6);
+                    lnodes + ((size_t)i << l) * 6, (int)threadIdx.x < nodes);
+    }
     __syncthreads();
   }
   if (threadIdx.x < 64) {  // root (slot 0) against the committed root: one 90-B compare, a wave's lanes

@@ -18,7 +18,7 @@ torch.cuda.set_device(dev)
 k, w = 128, 256
 NWG = w  # 2k trees... trees_lds: one workgroup per two trees -> 4k / 2 = 2w workgroups per block
 NWG = 2 * w
-trace = torch.zeros(NWG * 16 * 2, dtype=torch.int64, device=dev)
+trace = torch.zeros(NWG * 32 * 2, dtype=torch.int64, device=dev)
 os.environ["CDA_TREES_TRACE_PTR"] = str(trace.data_ptr())
 import bench  # noqa: E402
 import cda  # noqa: E402
@@ -38,27 +38,28 @@ for rep in range(12):
     s.synchronize()
     if rep < 2:
         continue
-    t = trace.cpu().numpy().reshape(NWG, 16, 2).astype(np.float64)
+    t = trace.cpu().numpy().reshape(NWG, 32, 2).astype(np.float64)
     rt, ck = t[:, :, 0], t[:, :, 1]
     ok = rt[:, 0] > 0
     t0 = rt[ok, 0].min()
-    last = int(np.argmax(rt[:, 14]))
-    row = {"entry_spread_us": float((rt[ok, 0].max() - t0) / 100), "leaf_load_us": float(np.median((rt[ok, 1] - rt[ok, 0]) / 100))}
-    lv, clk = [], []
+    last = int(np.argmax(rt[:, 29]))
+    med = lambda a: round(float(np.median(a)), 2)  # noqa: E731
+    row = {"leaf_load_us": med((rt[ok, 1] - rt[ok, 0]) / 100)}
+    prev = rt[ok, 1]
+    lv = []
     for l in range(1, 9):
-        d = (rt[ok, 1 + l] - rt[ok, l]) / 100
-        lv.append(round(float(np.median(d)), 2))
-        dc = (ck[ok, 1 + l] - ck[ok, l]) / np.maximum(1, (rt[ok, 1 + l] - rt[ok, l])) * 100  # MHz
-        clk.append(round(float(np.median(dc))))
+        a, b, c = rt[ok, 2 + 3 * (l - 1)], rt[ok, 3 + 3 * (l - 1)], rt[ok, 4 + 3 * (l - 1)]
+        if l == 1:
+            lv.append({"total": med((c - prev) / 100)})
+        else:
+            lv.append({"block0": med((a - prev) / 100), "barrier": med((b - a) / 100), "kw2": med((c - b) / 100),
+                       "total": med((c - prev) / 100)})
+        prev = c
     row["levels_us"] = lv
-    row["levels_clock_mhz"] = clk
-    row["digest_us"] = float(np.median((rt[ok, 11] - rt[ok, 9]) / 100))
-    row["counter_us"] = float(np.median((rt[ok, 12] - rt[ok, 11]) / 100))
-    row["last_wg_done_counter_us"] = float((rt[last, 12] - t0) / 100)
-    row["fold_wait_us"] = float((rt[last, 13] - rt[last, 12]) / 100)
-    row["fold_us"] = float((rt[last, 14] - rt[last, 13]) / 100)
-    row["fold_clock_mhz"] = float((ck[last, 14] - ck[last, 13]) / max(1, rt[last, 14] - rt[last, 13]) * 100)
-    row["total_us"] = float((rt[last, 14] - t0) / 100)
+    row["digest_us"] = med((rt[ok, 26] - prev) / 100)
+    row["counter_us"] = med((rt[ok, 27] - rt[ok, 26]) / 100)
+    row["fold_us"] = float((rt[last, 29] - rt[last, 28]) / 100)
+    row["total_us"] = float((rt[last, 29] - t0) / 100)
     out.append(row)
 best = min(out, key=lambda r: r["total_us"])
 worst = max(out, key=lambda r: r["total_us"])
