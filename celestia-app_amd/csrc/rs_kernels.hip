@@ -82,7 +82,8 @@ __device__ __forceinline__ void butterfly8(uint32_t* st, int mU, int U, int x, i
 }
 
 template <bool INVERSE>
-__device__ __forceinline__ void rs_layer8(uint32_t* st, int m, int U, int log2U, int D, int log2D) {
+__device__ __forceinline__ void rs_layer8(uint32_t* st, int m, int U, int log2U, int D, int log2D,
+                                          const unsigned long long* s_cb) {
   const int nbu = (m >> 1) << log2U;
   for (int bu = threadIdx.x; bu < nbu; bu += blockDim.x) {
     const int p = bu >> log2U, u = bu & (U - 1);
@@ -90,7 +91,15 @@ __device__ __forceinline__ void rs_layer8(uint32_t* st, int m, int U, int log2U,
     const int x = s0 | (p & (D - 1));
     const int y = x + D;
     const int idx = INVERSE ? (m - 1 + s0 + D) : (s0 + D - 1);
-    if ((D << log2U) >= 64) {  // constant is wave-uniform: masks in SGPRs
+    if (s_cb) {  // latency launches: the layer's matrix from the LDS copy (0 = no multiply)
+      unsigned long long cb = s_cb[idx];
+      if ((D << log2U) >= 64) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)cb);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(cb >> 32));
+        cb = (unsigned long long)hi << 32 | lo;
+      }
+      butterfly8<INVERSE>(st, m << log2U, U, x, y, u, cb ? 0u : 255u, cb);
+    } else if ((D << log2U) >= 64) {  // constant is wave-uniform: masks in SGPRs
       const int sidx = __builtin_amdgcn_readfirstlane(idx);
       const unsigned lm = c_skew8[sidx];
       butterfly8<INVERSE>(st, m << log2U, U, x, y, u, lm, c_col8[lm]);
@@ -110,6 +119,7 @@ struct Rs8Args {
   uint8_t* cpy;
   long long cpy_blk, cpy_cw, cpy_sh;
   int k, m, log2m, cw_per_blk, U, log2U, slices;
+  int lat;  // layer matrices staged in LDS at the start (small latency-bound launches; see launch_rs_encode8)
 };
 
 __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
@@ -125,6 +135,13 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
   uint8_t* dst = a.dst + blk * a.dst_blk + cw * a.dst_cw + byte_off;
   uint8_t* cpy = a.cpy ? a.cpy + blk * a.cpy_blk + cw * a.cpy_cw + byte_off : nullptr;
 
+  // per-index layer matrices c_col8[c_skew8[i]] (0 = no multiply) after the state: a per-lane constant is then one
+  // LDS read per layer instead of two dependent constant-memory loads
+  unsigned long long* s_cb = nullptr;
+  if (a.lat) {
+    s_cb = reinterpret_cast<unsigned long long*>(st + 8 * (a.m << a.log2U));
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_cb[i] = c_col8[c_skew8[i]];
+  }
   // load + bit-slice: element (s, u), s < m
   for (int e = threadIdx.x; e < (a.m << a.log2U); e += blockDim.x) {
     const int s = e >> a.log2U, u = e & (U - 1);
@@ -149,9 +166,9 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
   }
   __syncthreads();
   // IFFT (data at points m..m+k-1), D = 1 .. m/2
-  for (int lD = 0; lD < a.log2m; lD++) rs_layer8<true>(st, a.m, U, a.log2U, 1 << lD, lD);
+  for (int lD = 0; lD < a.log2m; lD++) rs_layer8<true>(st, a.m, U, a.log2U, 1 << lD, lD, s_cb);
   // FFT to points 0..k-1, D = m/2 .. 1
-  for (int lD = a.log2m - 1; lD >= 0; lD--) rs_layer8<false>(st, a.m, U, a.log2U, 1 << lD, lD);
+  for (int lD = a.log2m - 1; lD >= 0; lD--) rs_layer8<false>(st, a.m, U, a.log2U, 1 << lD, lD, s_cb);
   // un-slice + store parity
   for (int e = threadIdx.x; e < (a.k << a.log2U); e += blockDim.x) {
     const int s = e >> a.log2U, u = e & (U - 1);
@@ -587,8 +604,19 @@ static Rs8RegArgs reg_args(const RsJob& j) {
 int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   if (j.k < 1 || j.k > 128 || j.shard_len % 64 != 0) return -2;
   const int L = ilog2(j.k);
+  // Latency launches: when the register encoder's grid would leave most CUs idle (one block: 64 / 128 workgroups
+  // for rows / columns at k = 128, a consensus band 16), the LDS encoder splits each codeword's bytes over
+  // workgroups of U units (32 B each) instead, so the pass spreads over the chip.  CDA_RS8_LAT_U picks U
+  // (0 = off; default 4); results are identical either way (both encoders are bit-exact).
+  static const int lat_u = [] {
+    const char* e = getenv("CDA_RS8_LAT_U");
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
+  }();
+  const long long g2_grid = (long long)j.nblk * (j.cw_per_blk / 2) * (j.shard_len / 512);
+  const bool lat = lat_u && L >= 4 && j.shard_len % (32 * lat_u) == 0 && g2_grid < 32;
   // Batched path: 2 codewords per workgroup, register-resident (k >= 16).
-  if (L >= 4 && j.k % 2 == 0 && j.cw_per_blk % 2 == 0 && j.shard_len % 512 == 0) {
+  if (!lat && L >= 4 && j.k % 2 == 0 && j.cw_per_blk % 2 == 0 && j.shard_len % 512 == 0) {
     const Rs8RegArgs r = reg_args(j);
     const long long grid = (long long)j.nblk * r.groups_per_blk * r.slices;
     if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
@@ -621,12 +649,13 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   a.m = 1 << L;
   a.cw_per_blk = j.cw_per_blk;
   const int units = j.shard_len / 32;  // even
-  int U = 16;
+  int U = lat ? lat_u : 16;
   while (units % U) U >>= 1;
   a.U = U;
   a.log2U = ilog2(U);
   a.slices = units / U;
-  const size_t lds = (size_t)a.m * 8 * U * 4;
+  a.lat = lat ? 1 : 0;
+  const size_t lds = (size_t)a.m * 8 * U * 4 + (lat ? 256 * 8 : 0);
   const long long grid = (long long)j.nblk * j.cw_per_blk * a.slices;
   if (grid <= 0 || grid > 0x7FFFFFFF) return -2;
   hipLaunchKernelGGL(rs_encode8_kernel, dim3((unsigned)grid), dim3(256), lds, s, a);
@@ -739,6 +768,7 @@ struct Rs16Args {
   long long cpy_blk, cpy_cw, cpy_sh;
   const uint16_t* cpoly;  // [65536] per skew index: alpha^skew in std basis (0 = no multiply)
   int k, m, log2m, cw_per_blk, U, log2U, slices;
+  int lat;  // layer matrices staged in LDS at the start (small latency-bound launches; see launch_rs_encode8)
 };
 
 template <bool INVERSE>
