@@ -42,7 +42,14 @@ __device__ __forceinline__ int ns_cmp(const uint32_t* a, const uint32_t* b) {
 // ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share) ‖ 6 zero bytes, ns = share[0:29] if q0 else 0xFF×29.
 // Blocks 1..7 stay a loop (one copy of the compression code: measured as fast as
 // the unrolled form on MI355X, with half the instruction footprint).
+// The share is read one 128-B line at a time (two 64-B chunks loaded together, the odd chunk held in N until its
+// block): loaded a compression apart, the line's second half missed in L2 often enough that the leaf kernel fetched
+// 1.31x its bytes (all 128-B requests, profiles/r04_rdreq_sizes.json).  PAIRS = false: one chunk per block (16
+// fewer VGPRs; repair's root check, whose kernel would otherwise pass 128).
+template <bool PAIRS = true>
 __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q0, uint4* out) {
+  uint32_t N[16];
+  if (PAIRS) load16(sh + 4, N);  // chunk 1, the rest of the line A came from
   uint32_t ns[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) ns[i] = q0 ? A[i] : 0xFFFFFFFFu;
@@ -73,7 +80,15 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
 #pragma unroll 1
   for (int j = 1; j < 8; j++) {
     uint32_t C[16];
-    load16(sh + 4 * j, C);
+    if (!PAIRS) {
+      load16(sh + 4 * j, C);
+    } else if (j & 1) {  // odd chunk: loaded with the even one before it
+#pragma unroll
+      for (int i = 0; i < 16; i++) C[i] = N[i];
+    } else {
+      load16(sh + 4 * j, C);
+      load16(sh + 4 * (j + 1), N);
+    }
 #pragma unroll
     for (int i = 0; i < 7; i++) m[i] = be_window(H[i], H[i + 1], 2);
     m[7] = be_window(H[7], C[0], 2);

@@ -807,7 +807,7 @@ __global__ void __launch_bounds__(256) axes_verify_kernel(const uint8_t* __restr
       uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       if (ns_cmp(nb, A) < 0) bad = 1;
     }
-    leaf_record(sh, A, q0, lnodes + (size_t)i * 6);
+    leaf_record<false>(sh, A, q0, lnodes + (size_t)i * 6);
   }
   __syncthreads();
   for (int l = 1; l <= log2w; l++) {
