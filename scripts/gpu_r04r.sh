@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 4 final pass on the final code: GPU suite + smoke + rocprofv3 evidence (scripts/gpu_round.sh r04_v2), then
+# round 4 final pass on the final code: GPU suite + smoke + rocprofv3 evidence (scripts/gpu_round.sh $TAG, default r04_v2), then
 # the default bench line and the consensus probe.
 set -u
 mkdir -p gpurun_out
-bash scripts/gpu_round.sh r04_v2 > gpurun_out/r04r_round.log 2>&1
+bash scripts/gpu_round.sh ${TAG:-r04_v2} > gpurun_out/r04r_round.log 2>&1
 rc=$?; grep -E "^== |^rc=|passed|ABORT" gpurun_out/r04r_round.log; [ $rc -ne 0 ] && exit $rc
 grep -q ABORT gpurun_out/r04r_round.log && exit 1
 timeout -k 10 600 python -u bench.py > gpurun_out/r04r_bench.log 2>&1
