@@ -192,7 +192,10 @@ __device__ __forceinline__ void ld4(const uint4* p, uint32_t* w) {  // 4 x 16 B 
 // reads are neither merged nor hoisted and kept live, and each compression is
 // fenced: 89 VGPRs (5 waves/SIMD) instead of 205 when both children stayed in
 // registers.
-__device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po, bool store = true) {
+// ns_lds (optional): this thread's 128-B LDS slot; the first 64 B of both children are parked there when loaded for
+// blocks 0 / 1 and the namespace range is read back from it instead of from global memory.
+__device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po, bool store = true,
+                                              uint4* ns_lds = nullptr) {
   uint32_t st[8], m[16];
   sha256_init(st);
   // message = 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits); 48 words
@@ -202,12 +205,18 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
     m[0] = be_window(0x01000000u, L[0], 3);
 #pragma unroll
     for (int i = 1; i < 16; i++) m[i] = be_window(L[i - 1], L[i], 3);
+    if (ns_lds)
+#pragma unroll
+      for (int i = 0; i < 4; i++) ns_lds[i] = make_uint4(L[4 * i], L[4 * i + 1], L[4 * i + 2], L[4 * i + 3]);
   }
   sha256_compress_fenced(st, m);
   {  // block 1: words 16..31 <- L words 15..22, R words 0..8
     uint32_t L[16], R[16];  // L words 12..27, R words 0..15
     ld4(launder_after(pl, st[0]) + 3, L);  // words 12..27: only 12..23 are read
     ld4(launder_after(pr, st[0]), R);      // words 0..15: only 0..11 are read
+    if (ns_lds)
+#pragma unroll
+      for (int i = 0; i < 4; i++) ns_lds[4 + i] = make_uint4(R[4 * i], R[4 * i + 1], R[4 * i + 2], R[4 * i + 3]);
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int wi = 16 + i;
@@ -233,8 +242,17 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
 
   // namespace range: min = L.min; max = R.min == parity ns ? L.max : R.max
   uint32_t L[16], R[16];
-  ld4(launder_after(pl, st[0]), L);
-  ld4(launder_after(pr, st[0]), R);
+  if (ns_lds) {
+    uint32_t z = 0;  // an offset tied to the last compression keeps the LDS reads below it (pointer stays in LDS)
+    asm volatile("" : "+v"(z) : "v"(st[0]));
+    ld4(ns_lds + z, L);
+    ld4(ns_lds + z + 4, R);
+#pragma unroll
+    for (int i = 0; i < 16; i++) asm volatile("" : "+v"(L[i]), "+v"(R[i]));  // values, not a select of addresses
+  } else {
+    ld4(launder_after(pl, st[0]), L);
+    ld4(launder_after(pr, st[0]), R);
+  }
   bool rmin_max = true;
 #pragma unroll
   for (int i = 0; i < 7; i++) rmin_max &= (R[i] == 0xFFFFFFFFu);
