@@ -627,53 +627,113 @@ def host_path_measure(ctx, k, nblocks=48, reps=3):
 
 
 def one_block_fresh(ctx, ods, reps=25, warmup=3):
-    """The consensus call as go/cda.ExtendSharesOn makes it (go/cda/extend.go:42-48, app/process_proposal.go:137-151):
-    one k=128 block per cda_extend_commit_batch call, the shares freshly copied into a new flat buffer (outside the
-    timed call: Go's flatten runs before the cgo call) and a NEW, never-touched 32 MiB EDS buffer per call (np.empty:
-    fresh pages, as a large Go make()).  The buffers are allocated before and freed after the series: freeing a
-    32 MiB buffer unmaps it, a cost a Go caller's garbage collector pays elsewhere.  min / median / max over `reps`
-    calls after `warmup`; DAH checked, the EDS of the last call too."""
+    """The consensus call in the shapes go/cda makes it (app/prepare_proposal.go:65-93, app/process_proposal.go:137-151,
+    app/extend_block.go:25; go/cda/extend.go).  One k=128 block per cda_extend_commit_batch call; min / median / max
+    over `reps` calls after `warmup`; every DAH checked, and the EDS of the last call of each series.
+      roots_only            ProcessProposal / PrepareProposal through the roots-only entry (da.NewDataAvailability-
+                            HeaderFromShares, go/patches/0004): a fresh copy of the shares per call (np copy, outside
+                            the timed call, like the Go caller's own flatten), no EDS.
+      roots_only_pooled_in  the same with the shares flattened INTO a pooled page-locked slab inside the timed region
+                            (go/cda's share pool: the flatten the Go caller does anyway, then a direct DMA).
+      pooled_eds            ExtendShares / ExtendBlock (which must return the EDS): fresh shares (as roots_only), the
+                            EDS written into one of two recycled page-locked slabs (go/cda's EDS pool: Go-heap slabs
+                            registered once with cda_host_register and recycled through the garbage collector).
+      pooled_both           pooled shares slab (flatten inside the timed region) + pooled EDS slab.
+      with_eds              fresh shares and a NEW never-touched EDS buffer per call (np.empty, as a Go make()), no
+                            huge-page hint (the release default: the library does not change caller page policy).
+      with_eds_hugepages    the same on a context that opted in (cda_set_option(CDA_OPT_HUGE_PAGES, 1)).
+      pinned_with_eds       cda_host_alloc buffers reused across calls."""
+    import cda
+    from cda import _native as N
     k = int(round(len(ods) ** 0.5))
     eds_ref, _, _, dah_ref = ctx.extend_commit(ods)
     res = {}
-    for name, we in (("with_eds", True), ("roots_only", False)):
-        bufs = [np.empty((1, 4 * k * k, 512), np.uint8) for _ in range(warmup + reps)] if we else None
+
+    def series(name, call, check_eds=None):
         ts = []
         for i in range(warmup + reps):
-            src = ods.copy()[None]
+            prep = call(i)
             t0 = time.perf_counter()
-            _, _, _, dah = ctx.extend_commit_batch(src, want_eds=we, eds_out=bufs[i] if we else None)
+            dah = prep()
             el = (time.perf_counter() - t0) * 1e3
-            if bytes(dah[0]) != dah_ref:
-                raise RuntimeError("one-block DAH differs")
+            if bytes(dah) != dah_ref:
+                raise RuntimeError(f"one-block DAH differs ({name})")
             if i >= warmup:
                 ts.append(el)
-        if we and not np.array_equal(bufs[-1][0], eds_ref):
-            raise RuntimeError("one-block EDS differs")
-        del bufs
+        if check_eds is not None and not np.array_equal(check_eds(), eds_ref):
+            raise RuntimeError(f"one-block EDS differs ({name})")
         res[name] = {"ms_min": round(min(ts), 3), "ms_median": round(float(np.median(ts)), 3),
                      "ms_max": round(max(ts), 3), "median_over_min": round(float(np.median(ts)) / min(ts), 3)}
+
+    # roots only, fresh shares
+    def roots_fresh(i):
+        src = ods.copy()[None]
+        return lambda: ctx.extend_commit_batch(src, want_eds=False)[3][0]
+    series("roots_only", roots_fresh)
+    # pooled (registered) share slabs and EDS slabs, recycled round-robin like go/cda's pools
+    pool_in = [np.empty((1, k * k, 512), np.uint8) for _ in range(2)]
+    pool_out = [np.empty((1, 4 * k * k, 512), np.uint8) for _ in range(2)]
+    for b in pool_in + pool_out:
+        ctx.host_register(b)
+    try:
+        def roots_pooled_in(i):
+            slab = pool_in[i % 2]
+
+            def run():
+                np.copyto(slab[0], ods)  # the caller's flatten, into the pooled slab
+                return ctx.extend_commit_batch(slab, want_eds=False)[3][0]
+            return run
+        series("roots_only_pooled_in", roots_pooled_in)
+        last = {}
+
+        def pooled_eds(i):
+            src = ods.copy()[None]
+            out = pool_out[i % 2]
+            last["out"] = out
+            return lambda: ctx.extend_commit_batch(src, eds_out=out)[3][0]
+        series("pooled_eds", pooled_eds, lambda: last["out"][0])
+
+        def pooled_both(i):
+            slab, out = pool_in[i % 2], pool_out[i % 2]
+            last["out"] = out
+
+            def run():
+                np.copyto(slab[0], ods)
+                return ctx.extend_commit_batch(slab, eds_out=out)[3][0]
+            return run
+        series("pooled_both", pooled_both, lambda: last["out"][0])
+    finally:
+        for b in pool_in + pool_out:
+            ctx.host_unregister(b)
+    # fresh, never-touched EDS buffers (allocated before the series, kept alive: freeing unmaps them)
+    for name, c in (("with_eds", ctx), ("with_eds_hugepages", None)):
+        if c is None:
+            c = cda.Context(ctx.device)
+            c.set_option(N.OPT_HUGE_PAGES, 1)
+        bufs = [np.empty((1, 4 * k * k, 512), np.uint8) for _ in range(warmup + reps)]
+
+        def fresh(i, c=c, bufs=bufs):
+            src = ods.copy()[None]
+            return lambda: c.extend_commit_batch(src, eds_out=bufs[i])[3][0]
+        series(name, fresh, lambda bufs=bufs: bufs[-1][0])
+        del bufs
+        if c is not ctx:
+            c.close()
     # a caller that recycles pinned buffers (cda_host_alloc) for the shares and the EDS: both DMAs direct
     pb_ods, pb_eds = ctx.pinned((1, k * k, 512)), ctx.pinned((1, 4 * k * k, 512))
-    ts = []
-    for i in range(warmup + reps):
-        pb_ods.array[0] = ods
-        t0 = time.perf_counter()
-        _, _, _, dah = ctx.extend_commit_batch(pb_ods.array, eds_out=pb_eds.array)
-        el = (time.perf_counter() - t0) * 1e3
-        if bytes(dah[0]) != dah_ref:
-            raise RuntimeError("one-block DAH differs (pinned)")
-        if i >= warmup:
-            ts.append(el)
-    if not np.array_equal(pb_eds.array[0], eds_ref):
-        raise RuntimeError("one-block EDS differs (pinned)")
-    pb_ods.free()
-    pb_eds.free()
-    res["pinned_with_eds"] = {"ms_min": round(min(ts), 3), "ms_median": round(float(np.median(ts)), 3),
-                              "ms_max": round(max(ts), 3)}
-    res["note"] = (f"cda_extend_commit_batch, one k={k} block per call, a fresh untouched EDS buffer (np.empty) and a "
-                   f"fresh ODS copy per call; {warmup} untimed + {reps} timed calls; pinned_with_eds: cda_host_alloc "
-                   f"buffers reused across calls; csrc/consensus.cpp")
+    try:
+        def pinned(i):
+            pb_ods.array[0] = ods
+            return lambda: ctx.extend_commit_batch(pb_ods.array, eds_out=pb_eds.array)[3][0]
+        series("pinned_with_eds", pinned, lambda: pb_eds.array[0])
+    finally:
+        pb_ods.free()
+        pb_eds.free()
+    res["consensus_targets_ms"] = {"roots_only_median": 0.45, "pooled_eds_median": 0.70,
+                                   "source": "VERDICT r04 next #1 (driver BENCH line)"}
+    res["note"] = (f"cda_extend_commit_batch, one k={k} block per call, {warmup} untimed + {reps} timed calls per "
+                   f"series; csrc/consensus.cpp; pooled slabs: np.empty + cda_host_register, two per pool, "
+                   f"round-robin (go/cda/pool.go)")
     return res
 
 
@@ -763,6 +823,37 @@ def sum_over_ranks(x, world, backend, dev):
     t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def rank_report(world, rank, backend, dev, cpu_group, ms_per_step=None, blocks=None, check=None):
+    """Self-verification of a multi-rank run: `ranks_seen` = an all_reduce SUM of 1 over the
+    run's own process group (RCCL when one rank per GPU), and every rank's own step time, device and output check,
+    gathered over the CPU (gloo) group -- so the N-GPU line shows that each rank took part and on which GPU."""
+    import torch.distributed as dist
+    seen = sum_over_ranks(1.0, world, backend, dev)
+    mine = {"rank": rank, "host": os.uname().nodename, "pid": os.getpid()}
+    if dev is not None:
+        import torch
+        props = torch.cuda.get_device_properties(dev)
+        mine.update(device=dev.index, device_name=props.name,
+                    pci_bus_id=getattr(props, "pci_bus_id", None), pci_device_id=getattr(props, "pci_device_id", None),
+                    visible_devices=os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES"))
+    if ms_per_step is not None:
+        mine["ms_per_step"] = round(ms_per_step, 4)
+    if blocks is not None:
+        mine["blocks"] = blocks
+    if check is not None:
+        mine["blocks_checked_vs_golden"] = check.get("blocks_checked_vs_golden")
+    per = [mine]
+    if world > 1:
+        per = [None] * world
+        dist.all_gather_object(per, mine, group=cpu_group)
+    devs = [p.get("device") for p in per]
+    return {"ranks_seen": int(seen), "backend": backend, "per_rank": per,
+            "distinct_devices": len({(p.get("host"), p.get("pci_bus_id"), p.get("device")) for p in per})
+            if dev is not None else None,
+            "all_ranks_checked": all((p.get("blocks_checked_vs_golden") or 0) > 0 for p in per) if check else None,
+            "devices": devs}
 
 
 # ---- config C5's product path at N > 1: one k=512 square over all devices of the node, RCCL exchange ----------------
@@ -935,6 +1026,7 @@ def bench_main(args, world, rank, local, helper):
             dist.barrier()
         ranks = sum_over_ranks(1.0, world, backend, dev)
         t = max_over_ranks(float(rank), world, backend, dev)
+        rep = rank_report(world, rank, backend, dev, cpu_group, ms_per_step=float(rank), blocks=0)
         split = None
         if world > 1:
             dist.barrier(group=cpu_group)
@@ -943,7 +1035,8 @@ def bench_main(args, world, rank, local, helper):
             dist.barrier(group=cpu_group)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(ranks), "max_rank": int(t),
-                              "backend": backend, **({"k512_split": split} if split else {})}), flush=True)
+                              "backend": backend, "ranks": rep, **({"k512_split": split} if split else {})}),
+                  flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -981,6 +1074,7 @@ def bench_main(args, world, rank, local, helper):
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
+    mine_s = time.perf_counter() - t0  # this rank's own steps (before the closing barrier)
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, backend, dev)
@@ -990,6 +1084,8 @@ def bench_main(args, world, rank, local, helper):
     ms_per_step = 1000.0 * elapsed / args.steps
     # the timed steps' output: every block's DAH against the committed digests (tests/golden/bench_digests.json)
     check = check_dahs(d_dah.cpu().numpy(), k, B, rank, nd)
+    ranks_rep = rank_report(world, rank, backend, dev, cpu_group, ms_per_step=1000.0 * mine_s / args.steps,
+                            blocks=B * args.steps, check=check)
 
     # per-kernel durations: HIP events on the launch stream, separate pass (profiling adds event records)
     ctx.profile_reset()
@@ -1033,6 +1129,7 @@ def bench_main(args, world, rank, local, helper):
         "hbm_ceilings": ceil,
         "isa_mix_source": mix_src,
         "output_check": check,
+        "ranks": ranks_rep,
         "path_hbm_gbs": round(path_gbs, 1),
         "sha256_compressions_per_s": comp_per_s,
         "kernels_ms": {n: round(v["avg_ms"], 4) for n, v in kern.items()},
@@ -1161,8 +1258,9 @@ def gpu_vs_cpu(result, value):
         if hb.get("with_eds"):
             out["single_block_host_buffers_with_eds"] = round(best_cpu / hb["with_eds"], 1)
         fr = result.get("host_buffers", {}).get("one_block_fresh", {})
-        if fr.get("with_eds"):
-            out["single_block_fresh_buffers_with_eds_median"] = round(best_cpu / fr["with_eds"]["ms_median"], 1)
+        for key in ("roots_only", "pooled_eds", "pooled_both", "with_eds"):
+            if fr.get(key):
+                out[f"single_block_{key}_median"] = round(best_cpu / fr[key]["ms_median"], 1)
     c4 = cb.get("repair_c4_ms", {})
     g4 = result.get("repair_c4", {})
     for case in ("random", "q0_only"):

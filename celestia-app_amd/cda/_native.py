@@ -12,6 +12,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CDA_LIB: another build of the library (A/B measurements of kernel variants on one box)
 LIB_PATH = os.environ.get("CDA_LIB") or os.path.join(_HERE, "libcda.so")
+# the test-hooks build of the same sources (-DCDA_TEST_HOOKS=1, `make hooks`): failure injection through
+# CDA_FAULT_INJECT, which a release libcda.so ignores.  Only the fault tests load it, beside the release library.
+HOOKS_LIB_PATH = os.path.join(_HERE, "libcda_hooks.so")
 
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
@@ -52,8 +55,10 @@ EXPORTS = [
     "cda_host_alloc", "cda_host_free", "cda_multi_init", "cda_multi_free", "cda_multi_device_count",
     "cda_multi_context", "cda_multi_device", "cda_multi_extend_commit_batch", "cda_build_ods_device",
     "cda_construct_extend_commit", "cda_multi_extend_commit_split", "cda_multi_extend_commit_split_device",
-    "cda_multi_init_replicas",
+    "cda_multi_init_replicas", "cda_set_option", "cda_host_register", "cda_host_unregister",
 ]
+
+OPT_HUGE_PAGES = 1
 
 
 class ErrInfo(ctypes.Structure):
@@ -81,18 +86,18 @@ class CdaError(Exception):
         super().__init__(f"{msg or strerror(code)} (code {code}, axis {axis}, index {index}, leaf {leaf})")
 
 
-_lib = None
+_libs = {}
 _lib_lock = threading.Lock()
 
 
-def lib():
-    """Load libcda.so (raises if it was not built: no silent fallback)."""
-    global _lib
+def lib(path=None):
+    """Load libcda.so, or the build at `path` (raises if it was not built: no silent fallback)."""
+    path = path or LIB_PATH
     with _lib_lock:
-        if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise RuntimeError(f"libcda.so not built at {LIB_PATH}; run __graft_entry__.build()")
-            L = ctypes.CDLL(LIB_PATH)
+        if path not in _libs:
+            if not os.path.exists(path):
+                raise RuntimeError(f"libcda not built at {path}; run __graft_entry__.build()")
+            L = ctypes.CDLL(path)
             P, U32, I32, U64, I64, SZ = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64,
                                           ctypes.c_int64, ctypes.c_size_t)
             sig = {
@@ -139,18 +144,21 @@ def lib():
                 "cda_multi_init_replicas": (I32, [I32, U32, ctypes.POINTER(P)]),
                 "cda_build_ods_device": (I32, [P, U32, U32, P, P, U64, P, U32, P, P]),
                 "cda_construct_extend_commit": (I32, [P, U32, U32, P, P, U64, P, U32, P, P, P, P, P, P]),
+                "cda_set_option": (I32, [P, I32, I64]),
+                "cda_host_register": (I32, [P, P, SZ]),
+                "cda_host_unregister": (I32, [P, P]),
             }
             for name, (res, args) in sig.items():
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args
-            _lib = L
-    return _lib
+            _libs[path] = L
+    return _libs[path]
 
 
-def build_info():
-    """cda_build_info(): "release gfx950", or "diagnostic gfx950 <tags>" for a diagnostic library build."""
-    return lib().cda_build_info().decode()
+def build_info(path=None):
+    """cda_build_info(): "release gfx950", or "diagnostic gfx950 <tags>" for a diagnostic or test-hooks build."""
+    return lib(path).cda_build_info().decode()
 
 
 def strerror(code):
@@ -165,7 +173,7 @@ def _check(rc, err=None, ctx=None):
     if rc == OK:
         return
     if rc in (E_DEVICE, E_NOMEM, E_INTERNAL) and ctx is not None:
-        raise CdaError(rc, strerror(rc) + ": " + lib().cda_last_device_error(ctx._h).decode())
+        raise CdaError(rc, strerror(rc) + ": " + ctx._L.cda_last_device_error(ctx._h).decode())
     if err is not None:
         raise CdaError(rc, axis=err.axis, index=err.index, leaf=err.leaf, block=err.block)
     raise CdaError(rc)
@@ -178,9 +186,11 @@ class Context:
         """Pinned host buffer (cda_host_alloc) for the host-buffer batch path."""
         return PinnedBuffer(self, shape, dtype)
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, lib_path=None):
+        """lib_path: another build of libcda to bind this context to (the test-hooks library); default libcda.so."""
+        self._L = lib(lib_path)
         h = ctypes.c_void_p()
-        rc = lib().cda_init(device, ctypes.byref(h))
+        rc = self._L.cda_init(device, ctypes.byref(h))
         if rc != OK:
             raise CdaError(rc, "cda_init failed (no GPU visible?)")
         self._h = h
@@ -188,8 +198,19 @@ class Context:
 
     def close(self):
         if getattr(self, "_h", None) and not getattr(self, "_borrowed", False):  # a MultiContext's view: not ours
-            lib().cda_free(self._h)
+            self._L.cda_free(self._h)
         self._h = None
+
+    def set_option(self, option, value):
+        """cda_set_option (include/cda.h), e.g. OPT_HUGE_PAGES."""
+        _check(self._L.cda_set_option(self._h, option, int(value)), ctx=self)
+
+    def host_register(self, array):
+        """Page-lock a C-contiguous numpy array's memory for reuse as share / EDS buffers (cda_host_register)."""
+        _check(self._L.cda_host_register(self._h, array.ctypes.data_as(ctypes.c_void_p), array.nbytes), ctx=self)
+
+    def host_unregister(self, array):
+        _check(self._L.cda_host_unregister(self._h, array.ctypes.data_as(ctypes.c_void_p)), ctx=self)
 
     def __del__(self):
         try:
@@ -202,14 +223,14 @@ class Context:
         data = np.ascontiguousarray(data, np.uint8)
         k, L = data.shape
         parity = np.empty_like(data)
-        _check(lib().cda_rs_encode(self._h, k, L, _p(data), _p(parity)), ctx=self)
+        _check(self._L.cda_rs_encode(self._h, k, L, _p(data), _p(parity)), ctx=self)
         return parity
 
     def rs_decode(self, shards, present):
         sh = np.ascontiguousarray(shards, np.uint8).copy()
         pres = np.ascontiguousarray(present, np.uint8)
         n, L = sh.shape
-        _check(lib().cda_rs_decode(self._h, n // 2, L, _p(sh), _p(pres)), ctx=self)
+        _check(self._L.cda_rs_decode(self._h, n // 2, L, _p(sh), _p(pres)), ctx=self)
         return sh
 
     # ---- block path ----
@@ -222,7 +243,7 @@ class Context:
         cr = np.empty((2 * k, NODE_SIZE), np.uint8)
         dah = np.empty(32, np.uint8)
         err = ErrInfo()
-        rc = lib().cda_extend_commit(self._h, count, L, _p(shares), _p(eds), _p(rr), _p(cr), _p(dah),
+        rc = self._L.cda_extend_commit(self._h, count, L, _p(shares), _p(eds), _p(rr), _p(cr), _p(dah),
                                      ctypes.byref(err))
         _check(rc, err, self)
         return eds, rr, cr, dah.tobytes()
@@ -232,7 +253,7 @@ class Context:
         ods, k, eds, rr, cr, dah = _batch_outputs(ods, want_eds, eds_out)
         nb = len(ods)
         err = ErrInfo()
-        rc = lib().cda_extend_commit_batch(self._h, k, nb, _p(ods), _p(eds), _p(rr), _p(cr), _p(dah),
+        rc = self._L.cda_extend_commit_batch(self._h, k, nb, _p(ods), _p(eds), _p(rr), _p(cr), _p(dah),
                                            ctypes.byref(err))
         _check(rc, err, self)
         return eds, rr, cr, dah
@@ -250,38 +271,38 @@ class Context:
         cr = np.empty((w, NODE_SIZE), np.uint8)
         dah = np.empty(32, np.uint8)
         err = ErrInfo()
-        rc = lib().cda_construct_extend_commit(self._h, k, len(recs), ctypes.cast(recs, ctypes.c_void_p), _p(data),
+        rc = self._L.cda_construct_extend_commit(self._h, k, len(recs), ctypes.cast(recs, ctypes.c_void_p), _p(data),
                                                sum(r.data_len for r in recs), _p(reserved), len(reserved), _p(ods),
                                                _p(eds), _p(rr), _p(cr), _p(dah), ctypes.byref(err))
         _check(rc, err, self)
         return ods, eds, rr, cr, dah.tobytes()
 
     def extend_commit_device(self, k, nblocks, d_ods, d_eds, d_roots, d_dah, d_status, stream=None):
-        rc = lib().cda_extend_commit_device(self._h, k, nblocks, ctypes.c_void_p(d_ods), ctypes.c_void_p(d_eds),
+        rc = self._L.cda_extend_commit_device(self._h, k, nblocks, ctypes.c_void_p(d_ods), ctypes.c_void_p(d_eds),
                                             ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
                                             ctypes.c_void_p(d_status), ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
 
     # ---- device-resident building blocks (pointers are device addresses) ----
     def rs_encode_device(self, k, shard_len, ncw, d_src, src_cw, src_sh, d_dst, dst_cw, dst_sh, stream=None):
-        rc = lib().cda_rs_encode_device(self._h, k, shard_len, ncw, ctypes.c_void_p(d_src), src_cw, src_sh,
+        rc = self._L.cda_rs_encode_device(self._h, k, shard_len, ncw, ctypes.c_void_p(d_src), src_cw, src_sh,
                                         ctypes.c_void_p(d_dst), dst_cw, dst_sh, ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
 
     def nmt_roots_device(self, k, d_eds, axis, first_index, naxes, leaf_off, nleaves, d_roots, d_status,
                          stream=None):
-        rc = lib().cda_nmt_roots_device(self._h, k, ctypes.c_void_p(d_eds), axis, first_index, naxes, leaf_off,
+        rc = self._L.cda_nmt_roots_device(self._h, k, ctypes.c_void_p(d_eds), axis, first_index, naxes, leaf_off,
                                         nleaves, ctypes.c_void_p(d_roots), ctypes.c_void_p(d_status),
                                         ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
 
     def nmt_fold_device(self, ntrees, n, d_nodes, d_roots, stream=None):
-        rc = lib().cda_nmt_fold_device(self._h, ntrees, n, ctypes.c_void_p(d_nodes), ctypes.c_void_p(d_roots),
+        rc = self._L.cda_nmt_fold_device(self._h, ntrees, n, ctypes.c_void_p(d_nodes), ctypes.c_void_p(d_roots),
                                        ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
 
     def dah_device(self, n_total, d_roots, d_dah, stream=None):
-        rc = lib().cda_dah_device(self._h, n_total, ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
+        rc = self._L.cda_dah_device(self._h, n_total, ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
                                   ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
 
@@ -292,7 +313,7 @@ class Context:
         cr = np.empty((w, NODE_SIZE), np.uint8)
         dah = np.empty(32, np.uint8)
         err = ErrInfo()
-        _check(lib().cda_commit_eds(self._h, w // 2, _p(eds), _p(rr), _p(cr), _p(dah), ctypes.byref(err)), err, self)
+        _check(self._L.cda_commit_eds(self._h, w // 2, _p(eds), _p(rr), _p(cr), _p(dah), ctypes.byref(err)), err, self)
         return rr, cr, dah.tobytes()
 
     def dah_hash(self, row_roots, col_roots):
@@ -300,7 +321,7 @@ class Context:
         rr = np.ascontiguousarray(np.asarray(row_roots, np.uint8).reshape(n, NODE_SIZE)) if n else None
         cr = np.ascontiguousarray(np.asarray(col_roots, np.uint8).reshape(n, NODE_SIZE)) if n else None
         out = np.empty(32, np.uint8)
-        _check(lib().cda_dah_hash(self._h, n, _p(rr), _p(cr), _p(out)), ctx=self)
+        _check(self._L.cda_dah_hash(self._h, n, _p(rr), _p(cr), _p(out)), ctx=self)
         return out.tobytes()
 
     def nmt_axis_root(self, square_size, axis_index, leaves):
@@ -315,7 +336,7 @@ class Context:
             leaf_len, buf = 0, None
         root = np.empty(NODE_SIZE, np.uint8)
         err = ErrInfo()
-        rc = lib().cda_nmt_axis_root(self._h, square_size, axis_index, n, leaf_len, _p(buf), _p(root),
+        rc = self._L.cda_nmt_axis_root(self._h, square_size, axis_index, n, leaf_len, _p(buf), _p(root),
                                      ctypes.byref(err))
         _check(rc, err, self)
         return root.tobytes()
@@ -341,7 +362,7 @@ class Context:
         if eds.shape[0] != w * w or eds.size != w * w * SHARE_SIZE or pres.size != w * w:
             raise CdaError(E_ARG, "eds must be (2k)^2 x 512 bytes and present (2k)^2 flags")
         err = ErrInfo()
-        rc = lib().cda_repair(self._h, w // 2, _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots, np.uint8)),
+        rc = self._L.cda_repair(self._h, w // 2, _p(eds), _p(pres), _p(np.ascontiguousarray(row_roots, np.uint8)),
                               _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err))
         return rc, eds, pres, err
 
@@ -353,7 +374,7 @@ class Context:
         if pres.size != w * w or len(row_roots) != w or len(col_roots) != w:
             raise CdaError(E_ARG, "present must hold (2k)^2 flags and the roots 2k entries each")
         err = ErrInfo()
-        rc = lib().cda_repair_device(self._h, k, ctypes.c_void_p(d_eds), _p(pres),
+        rc = self._L.cda_repair_device(self._h, k, ctypes.c_void_p(d_eds), _p(pres),
                                      _p(np.ascontiguousarray(row_roots, np.uint8)),
                                      _p(np.ascontiguousarray(col_roots, np.uint8)), ctypes.byref(err),
                                      ctypes.c_void_p(stream or 0))
@@ -380,7 +401,7 @@ class Context:
         nb = len(offsets) - 1
         out = np.empty((nb, 32), np.uint8)
         err = ErrInfo()
-        rc = lib().cda_blob_commitments(self._h, nb, _p(namespaces), _p(data), _p(offsets), _p(share_versions),
+        rc = self._L.cda_blob_commitments(self._h, nb, _p(namespaces), _p(data), _p(offsets), _p(share_versions),
                                         subtree_root_threshold, _p(out), ctypes.byref(err))
         _check(rc, err, self)
         return out
@@ -392,7 +413,7 @@ class Context:
         flat = b"".join(bytes(x) for st in sets for x in st)
         items = np.frombuffer(flat, np.uint8).copy() if flat else None
         out = np.empty((len(sets), 32), np.uint8)
-        _check(lib().cda_merkle_roots(self._h, len(sets), _p(offs), _p(items), NODE_SIZE, _p(out)), ctx=self)
+        _check(self._L.cda_merkle_roots(self._h, len(sets), _p(offs), _p(items), NODE_SIZE, _p(out)), ctx=self)
         return [bytes(o) for o in out]
 
     def extend_commit_nodes(self, shares, want_eds=False, rows=True, cols=True, dah_tree=True):
@@ -407,7 +428,7 @@ class Context:
         cn = np.empty((w, 2 * w - 1, NODE_SIZE), np.uint8) if cols else None
         dn = np.empty((4 * w - 1, 32), np.uint8) if dah_tree else None
         err = ErrInfo()
-        rc = lib().cda_extend_commit_nodes(self._h, count, L, _p(shares), _p(eds), _p(rr), _p(cr), _p(dah), _p(rn),
+        rc = self._L.cda_extend_commit_nodes(self._h, count, L, _p(shares), _p(eds), _p(rr), _p(cr), _p(dah), _p(rn),
                                            _p(cn), _p(dn), ctypes.byref(err))
         _check(rc, err, self)
         return {"eds": eds, "row_roots": rr, "col_roots": cr, "dah": dah.tobytes(), "row_nodes": rn,
@@ -426,7 +447,7 @@ class Context:
         nodes = np.empty((k, 2 * lg, NODE_SIZE), np.uint8)
         root = np.empty(32, np.uint8)
         err = ErrInfo()
-        rc = lib().cda_share_inclusion_proof(self._h, count, L, _p(shares), start, end, ctypes.byref(info), _p(rr),
+        rc = self._L.cda_share_inclusion_proof(self._h, count, L, _p(shares), start, end, ctypes.byref(info), _p(rr),
                                              _p(lh), _p(au), _p(ns), _p(ne), _p(nc), _p(nodes), _p(root),
                                              ctypes.byref(err))
         _check(rc, err, self)
@@ -438,17 +459,17 @@ class Context:
 
     # ---- profiling ----
     def profile_enable(self, on=True):
-        _check(lib().cda_profile_enable(self._h, 1 if on else 0), ctx=self)
+        _check(self._L.cda_profile_enable(self._h, 1 if on else 0), ctx=self)
 
     def profile_reset(self):
-        _check(lib().cda_profile_reset(self._h), ctx=self)
+        _check(self._L.cda_profile_reset(self._h), ctx=self)
 
     def profile_read(self):
         cap = 64
         names = ctypes.create_string_buffer(4096)
         ms = np.zeros(cap, np.float64)
         cnt = np.zeros(cap, np.int64)
-        n = lib().cda_profile_read(self._h, names, 4096, _p(ms), _p(cnt), cap)
+        n = self._L.cda_profile_read(self._h, names, 4096, _p(ms), _p(cnt), cap)
         out, parts = {}, names.raw.split(b"\0")
         for i in range(n):
             out[parts[i].decode()] = (float(ms[i]), int(cnt[i]))
@@ -486,14 +507,14 @@ class PinnedBuffer:
     def __init__(self, ctx, shape, dtype=np.uint8):
         nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
         ptr = ctypes.c_void_p()
-        _check(lib().cda_host_alloc(ctx._h, nbytes, ctypes.byref(ptr)), ctx=ctx)
+        _check(ctx._L.cda_host_alloc(ctx._h, nbytes, ctypes.byref(ptr)), ctx=ctx)
         self._ctx, self._ptr = ctx, ptr
         buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(ptr.value)
         self.array = np.frombuffer(buf, np.uint8, count=nbytes).view(dtype).reshape(shape)
 
     def free(self):
         if self._ptr is not None and self._ctx._h:
-            lib().cda_host_free(self._ctx._h, self._ptr)
+            self._ctx._L.cda_host_free(self._ctx._h, self._ptr)
         self._ptr = None
 
     def __del__(self):
@@ -528,6 +549,7 @@ class MultiContext:
     def context(self, i):
         """Context view of device i's cda_ctx (owned by this handle)."""
         c = Context.__new__(Context)
+        c._L = lib()
         c._h = ctypes.c_void_p(lib().cda_multi_context(self._h, i))
         c.device = lib().cda_multi_device(self._h, i)
         c._borrowed = True

@@ -127,8 +127,13 @@ def validate_blobs(blobs):
 
 
 def _batchable(blobs):
-    return bool(blobs) and all(len(b["ns"]) == appconsts.NAMESPACE_SIZE and b["data"] and
-                               b["share_version"] in appconsts.SUPPORTED_SHARE_VERSIONS for b in blobs)
+    """A BlobTx's blobs enter the batched commitment call exactly when ValidateBlobs accepts them (the filter of the
+    Go patch's PrecomputeCommitments: reserved namespaces, namespace version and the v0 prefix included)."""
+    try:
+        validate_blobs(blobs)
+    except BlobTxError:
+        return False
+    return True
 
 
 def precompute_commitments(txs, subtree_root_threshold=appconsts.SUBTREE_ROOT_THRESHOLD, ctx=None):

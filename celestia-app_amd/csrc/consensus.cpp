@@ -210,9 +210,8 @@ int get_consensus(cda_ctx* c, Consensus*& out) {
   }
   if (!c->cons->pool) {
     fault_point("thread");
-    int n = 7;  // + the calling thread; measured: scripts/consensus_probe.py
-    if (const char* e = getenv("CDA_COPY_THREADS")) n = std::max(1, std::min(64, atoi(e)));
-    c->cons->pool = new CopyPool(c, n);
+    // 7 + the calling thread by default (measured: scripts/consensus_probe.py); CDA_COPY_THREADS read at cda_init
+    c->cons->pool = new CopyPool(c, c->copy_threads);
   }
   out = c->cons;
   return CDA_OK;
@@ -267,10 +266,11 @@ bool pages_resident(const uint8_t* p, size_t n) {
   return true;
 }
 
-// Fresh output: ask for transparent huge pages on its 2 MiB-aligned interior before anything touches it.  The GPU box
-// runs THP in "madvise" mode; with 4 KiB pages the first-touch faults of 32 MiB did not scale past ~14 GB/s over any
-// number of threads, with huge pages 8 threads wrote fresh memory at ~58 GB/s (tools/fault_probe.cpp,
-// profiles/r04_pass1.log).  A hint on the caller's range: it changes page size, never contents.
+// Fresh output, opt-in only (cda_set_option(CDA_OPT_HUGE_PAGES)): ask for transparent huge pages on its 2 MiB-aligned
+// interior before anything touches it.  The GPU box runs THP in "madvise" mode; with 4 KiB pages the first-touch
+// faults of 32 MiB did not scale past ~14 GB/s over any number of threads, with huge pages 8 threads wrote fresh memory
+// at ~58 GB/s (tools/fault_probe.cpp, profiles/r04_pass1.log).  It changes page size, never contents -- but it is a
+// page policy on memory the library does not own (a Go heap span under cgo), so it is not the default.
 void want_huge_pages(uint8_t* p, size_t n) {
   const uintptr_t lo = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
   const uintptr_t hi = ((uintptr_t)p + n) & ~(uintptr_t)((2u << 20) - 1);
@@ -299,14 +299,13 @@ void want_huge_pages(uint8_t* p, size_t n) {
 //               per block, r04_pass1); sending the bottom half through the pinned slab in 1 MiB chunks copied out by
 //               the pool took 1.02-1.23 ms against 0.80-0.88 ms for this form (r04_pass4.log); registering it
 //               (hipHostRegister, async DMA, unregister) was no faster.
-// Q0 is always the host copy of the caller's shares.  A/B knobs (read per call): CDA_CONS_IN = 1 (bands) /
-// 2 (one copy), CDA_CONS_OUT = 2 (the resident form on any pageable buffer), CDA_CONS_TRACE (phase timestamps).
+// Q0 is always the host copy of the caller's shares.  A/B forms (ctx fields read once at cda_init, ctx.h):
+// cons_in = 1 (bands) / 2 (one copy), cons_out = 2 (the resident form on any pageable buffer), cons_trace (phase
+// timestamps), cons_stg_mib.  A fresh output gets the huge-page hint only when the caller opted in (huge_pages).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
-  const char* e_in = getenv("CDA_CONS_IN");  // read per call: the tests switch forms within one process
-  const char* e_out = getenv("CDA_CONS_OUT");
-  const int in_mode_env = e_in ? atoi(e_in) : 0, out_mode = e_out ? atoi(e_out) : 0;
-  const bool trace = getenv("CDA_CONS_TRACE") != nullptr;
+  const int in_mode_env = c->cons_in, out_mode = c->cons_out;
+  const bool trace = c->cons_trace;
   double tr[8] = {0};
   const auto t_start = std::chrono::steady_clock::now();
   auto mark = [&](int i) {
@@ -321,7 +320,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   int rc;
   if ((rc = ensure_pipeline(c)) || (rc = get_consensus(c, X)) || (rc = ensure(c, c->ods, ods_b)) ||
       (rc = ensure(c, c->eds, eds_b)) || (rc = ensure(c, c->leaf, cells * CDA_REC_BYTES)) ||
-      (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)))
+      (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)) || (rc = prepare_trees(c, k, 1, c->stream)))
     return rc;
   const bool want = eds_or_null != nullptr;
   const bool out_pinned = want && pinned_host(eds_or_null);
@@ -333,16 +332,15 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   // pageable DMA alone ran at 36-46 GB/s; side by side the two fill the link.  Staged share, same box
   // (r04_pass12..14.log, k = 128, 16 MiB bottom half): fresh output 0 / 6 / 8 / 10 / 12 MiB -> 0.86 / 0.77 / 0.755
   // / 0.84 / 0.86-0.97 ms, written output 0 / 6 / 8 MiB -> 0.73 / 0.71 / 0.77 ms; so half for a fresh buffer,
-  // 3/8 for a written one.  CDA_CONS_STG = MiB to stage instead (0: all pageable; A/B runs).
-  const char* e_stg = getenv("CDA_CONS_STG");
-  const size_t stg_want = e_stg ? ((size_t)std::max(0, atoi(e_stg)) << 20) : (fresh ? bot_b / 2 : bot_b / 8 * 3);
+  // 3/8 for a written one.  cons_stg_mib (CDA_CONS_STG) = MiB to stage instead (0: all pageable; A/B runs).
+  const size_t stg_want = c->cons_stg_mib >= 0 ? ((size_t)c->cons_stg_mib << 20) : (fresh ? bot_b / 2 : bot_b / 8 * 3);
   const size_t stg_b = (want && !out_pinned) ? std::min(bot_b / 4 * 3, stg_want / (2 * erowS) * (2 * erowS)) : 0;
   const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
   const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
   if ((want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
       (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
     return rc;
-  if (fresh) want_huge_pages(eds_or_null, eds_b);
+  if (fresh && c->huge_pages) want_huge_pages(eds_or_null, eds_b);  // opt-in only (cda_set_option)
   uint8_t* d_ods = (uint8_t*)c->ods.p;
   uint8_t* d_eds = (uint8_t*)c->eds.p;
   uint8_t* d_roots = X->d_res;
@@ -404,6 +402,23 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
     }
   }
   X->pool->start(&tasks);
+  // From here the pool's tasks reference this frame (tasks, touched, the counters, abort) and the caller's buffers:
+  // on ANY exit before the orderly join below -- an error return or an exception -- the guard stops them, joins the
+  // job and drains the three streams before those locals (declared above it) are destroyed.
+  struct JoinGuard {
+    cda_ctx* c;
+    Consensus* X;
+    std::atomic<bool>& abort;
+    bool armed = true;
+    ~JoinGuard() {
+      if (!armed) return;
+      abort.store(true);
+      X->pool->help_and_wait();
+      (void)hipStreamSynchronize(c->h2d_stream);
+      (void)hipStreamSynchronize(c->stream);
+      (void)hipStreamSynchronize(c->d2h_stream);
+    }
+  } guard{c, X, abort};
   mark(1);
 
   hipStream_t s = c->stream;
@@ -499,6 +514,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   mark(4);
   if (fail) abort.store(true);
   X->pool->help_and_wait();
+  guard.armed = false;  // joined here; the streams are waited for below on every path
   mark(5);
   if (!fail) wait_event(X->ev_done, abort);
   mark(6);

@@ -71,6 +71,18 @@ struct cda_ctx {
   // one-block calls down the serial form instead (A/B runs)
   cda::Consensus* cons = nullptr;
   bool consensus = true;
+  // A/B forms of the one-block path, read ONCE at cda_init (never per call: glibc getenv is not safe against a Go
+  // runtime's concurrent setenv, and the environment must not steer a running node's path).  cons_in: 0 = default,
+  // 1 = four input bands, 2 = one copy (CDA_CONS_IN); cons_out: 2 = the resident-buffer form on any pageable output
+  // (CDA_CONS_OUT); cons_stg_mib: MiB of the bottom half staged through the pinned slab, -1 = default (CDA_CONS_STG);
+  // cons_trace: phase timestamps to stderr (CDA_CONS_TRACE); copy_threads: pool size (CDA_COPY_THREADS).
+  int cons_in = 0, cons_out = 0, cons_stg_mib = -1, copy_threads = 7;
+  bool cons_trace = false;
+  // Transparent huge pages for a fresh (never-touched) caller output buffer: madvise(MADV_HUGEPAGE) on its 2 MiB-aligned
+  // interior before the copy pool touches it.  OFF by default: the hint changes the page policy of memory
+  // the library does not own -- under cgo, Go heap.  Opt in per context with cda_set_option(CDA_OPT_HUGE_PAGES, 1) or
+  // CDA_HUGE_PAGES=1 at cda_init.  A caller that recycles pinned buffers (go/cda's EDS pool) never takes this path.
+  bool huge_pages = false;
   // profiling
   bool prof = false;
   struct Pending {
@@ -135,6 +147,8 @@ RsJob cols_job(uint32_t k, uint32_t nblocks, uint8_t* d_eds);
 // words are set to "no error" first unless the caller already did (init_status = false)
 int enqueue_commit(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_eds, void* d_roots, void* d_dah,
                    unsigned long long* d_status, hipStream_t s, size_t rec_off, bool init_status = true);
+// grow the tree phase's counters / digest scratch for (k, nblocks) before its launch (engine.cpp)
+int prepare_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, hipStream_t s);
 // RS phase of the block pipeline: rows (Q0 copy + Q1) then columns (Q2|Q3) of nblocks blocks.
 int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds, hipStream_t s);
 // split_kernels.hip
@@ -151,10 +165,19 @@ int launch_tree_roots(const TreeSpec* spec, int nsets, int log2n, hipStream_t s)
 // entry point wraps its body in CDA_API_TRY / CDA_API_CATCH(ctx): std::bad_alloc -> CDA_E_NOMEM, anything else
 // (std::system_error from a thread start, ...) -> CDA_E_INTERNAL, with what() in cda_last_device_error.
 int api_exception(cda_ctx* c) noexcept;  // call from a catch block: classifies the exception in flight
-// Failure injection for tests: CDA_FAULT_INJECT=<site> throws at that site -- "entry" (every entry point, before
-// its body), "alloc" (device workspace growth, as std::bad_alloc), "thread" (a helper-thread start, as
-// std::system_error).  Unset in production; one getenv per call.
+// Failure injection, TEST BUILDS ONLY (-DCDA_TEST_HOOKS=1: `make hooks` -> cda/libcda_hooks.so, loaded by the fault
+// tests through CDA_LIB): CDA_FAULT_INJECT=<site> throws at that site -- "entry" (every entry point, before its
+// body), "alloc" (device workspace growth, as std::bad_alloc), "thread" (a helper-thread start, as
+// std::system_error).  In a release library fault_point is an empty inline function: no environment variable can
+// make a release build fail; cda_build_info() names a hooks build.
+#ifndef CDA_TEST_HOOKS
+#define CDA_TEST_HOOKS 0
+#endif
+#if CDA_TEST_HOOKS
 void fault_point(const char* site);
+#else
+inline void fault_point(const char*) {}
+#endif
 #define CDA_API_TRY try { ::cda::fault_point("entry");
 #define CDA_API_CATCH(ctx) \
   }                        \

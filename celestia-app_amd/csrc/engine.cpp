@@ -90,6 +90,7 @@ int api_exception(cda_ctx* c) noexcept {
   return code;
 }
 
+#if CDA_TEST_HOOKS
 void fault_point(const char* site) {
   const char* e = getenv("CDA_FAULT_INJECT");
   if (!e || strcmp(e, site) != 0) return;
@@ -97,6 +98,7 @@ void fault_point(const char* site) {
     throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again), "injected thread failure");
   throw std::bad_alloc();
 }
+#endif
 
 int ensure(cda_ctx* c, cda_ctx::Buf& b, size_t bytes) {
   if (b.cap >= bytes) return CDA_OK;
@@ -206,17 +208,28 @@ int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, u
 
 // Commitment phase: leaf hashing, NMT levels, DAH of nblocks extended blocks.
 // NMT levels + DAH of nblocks blocks whose leaf records are at record offset rec_off.
+// small batches (latency: the consensus path extends one block): all trees + the DAH in one LDS-resident launch
+static bool lds_trees_path(uint32_t k, uint32_t nblocks) {
+  static const int lds_trees = getenv("CDA_TREES_LDS") ? atoi(getenv("CDA_TREES_LDS")) : kLdsTreesMax;  // once
+  return (size_t)nblocks * 4 * k <= (size_t)lds_trees && 2 * k <= 256;
+}
+
+// The tree phase's per-block counters (zeroed once; the kernels leave them at 0) and digest scratch, grown before
+// any work that must not be interrupted is started (the one-block path's copy pool, consensus.cpp).
+int prepare_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, hipStream_t s) {
+  if (!lds_trees_path(k, nblocks) && 2 * k < 1024) return CDA_OK;  // level kernels + dah_kernel: no scratch
+  const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255, need = cnt_b + (size_t)nblocks * 4 * k * 32;
+  if (c->done.cap >= need) return CDA_OK;
+  int rc = ensure(c, c->done, std::max<size_t>(need, 64 * 1024));
+  if (rc) return rc;
+  return dev_ok(c, hipMemsetAsync(c->done.p, 0, c->done.cap, s), "hipMemsetAsync") ? CDA_OK : CDA_E_DEVICE;
+}
+
 int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void* d_dah, hipStream_t s, size_t rec_off) {
   const uint32_t w = 2 * k;
-  // small batches (latency: the consensus path extends one block): all trees + the DAH in one LDS-resident launch
-  static const int lds_trees = getenv("CDA_TREES_LDS") ? atoi(getenv("CDA_TREES_LDS")) : kLdsTreesMax;
-  if ((size_t)nblocks * 2 * w <= (size_t)lds_trees && w <= 256) {
-    const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255, need = cnt_b + (size_t)nblocks * 2 * w * 32;
-    if (c->done.cap < need) {  // counters zeroed once (the kernel leaves them at 0), then the digest scratch
-      int rc = ensure(c, c->done, std::max<size_t>(need, 64 * 1024));
-      if (rc) return rc;
-      if (!dev_ok(c, hipMemsetAsync(c->done.p, 0, c->done.cap, s), "hipMemsetAsync")) return CDA_E_DEVICE;
-    }
+  if (lds_trees_path(k, nblocks)) {
+    const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255;
+    if (int rc = prepare_trees(c, k, nblocks, s)) return rc;
     ProfScope ps(c, "trees_lds", s);
     const int lr = launch_trees_lds((uint8_t*)c->leaf.p + rec_off * CDA_REC_BYTES, d_roots, d_dah,
                                     (unsigned*)c->done.p, (uint8_t*)c->done.p + cnt_b, (int)k, (int)nblocks, s);
@@ -236,12 +249,8 @@ int enqueue_trees(cda_ctx* c, uint32_t k, uint32_t nblocks, void* d_roots, void*
   } else {  // k = 512: 2,048 roots, 8 digest compressions per thread in one workgroup -> 2 over eight (0.147 ->
             // 0.112 ms per two squares)
     // per-block counters (zeroed once; the kernel leaves them at 0), then n digests of 32 B per block
-    const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255, need = cnt_b + (size_t)nblocks * 2 * w * 32;
-    if (c->done.cap < need) {
-      int rc = ensure(c, c->done, std::max<size_t>(need, 64 * 1024));
-      if (rc) return rc;
-      if (!dev_ok(c, hipMemsetAsync(c->done.p, 0, c->done.cap, s), "hipMemsetAsync")) return CDA_E_DEVICE;
-    }
+    const size_t cnt_b = ((size_t)nblocks * 4 + 255) & ~(size_t)255;
+    if (int rc = prepare_trees(c, k, nblocks, s)) return rc;
     ProfScope ps(c, "dah", s);
     const int lr = launch_dah_wide(d_roots, d_dah, (unsigned*)c->done.p, (uint8_t*)c->done.p + cnt_b, (int)(2 * w),
                                    (int)nblocks, s);
@@ -324,6 +333,13 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
   if (const char* e = getenv("CDA_STAGING")) c->staging = atoi(e) & 3;
   if (const char* e = getenv("CDA_CONSENSUS")) c->consensus = atoi(e) != 0;
+  // the one-block path's A/B forms and the huge-page opt-in: read here once, never per call (ctx.h)
+  if (const char* e = getenv("CDA_CONS_IN")) c->cons_in = std::max(0, std::min(2, atoi(e)));
+  if (const char* e = getenv("CDA_CONS_OUT")) c->cons_out = atoi(e) == 2 ? 2 : 0;
+  if (const char* e = getenv("CDA_CONS_STG")) c->cons_stg_mib = std::max(0, atoi(e));
+  if (const char* e = getenv("CDA_COPY_THREADS")) c->copy_threads = std::max(1, std::min(64, atoi(e)));
+  if (const char* e = getenv("CDA_HUGE_PAGES")) c->huge_pages = atoi(e) != 0;
+  c->cons_trace = getenv("CDA_CONS_TRACE") != nullptr;
   find_local_cpus(c);
   // the streams that overlap each other, created right after `stream` so that they land on distinct hardware
   // queues (HIP assigns streams to its GPU_MAX_HW_QUEUES = 4 queues round-robin)
@@ -398,11 +414,22 @@ const char* cda_last_device_error(cda_ctx* c) { return c ? c->last_err.c_str() :
 const char* cda_build_info(void) {
   static const std::string info = [] {
     std::string d;
-    for (const char* t : {rs8_diag_tag(), rs16_diag_tag()})
+    for (const char* t : {rs8_diag_tag(), rs16_diag_tag(), CDA_TEST_HOOKS ? "test_hooks" : ""})
       if (*t) d += (d.empty() ? "" : ",") + std::string(t);
     return d.empty() ? std::string("release gfx950") : "diagnostic gfx950 " + d;
   }();
   return info.c_str();
+}
+
+int cda_set_option(cda_ctx* c, int option, int64_t value) {
+  CDA_API_TRY
+  if (!c) return CDA_E_ARG;
+  Lock l(c);
+  switch (option) {
+    case CDA_OPT_HUGE_PAGES: c->huge_pages = value != 0; return CDA_OK;
+    default: return CDA_E_ARG;
+  }
+  CDA_API_CATCH(c)
 }
 
 int64_t cda_rs_max_chunks(void) { return (int64_t)32768 * 32768; }

@@ -258,6 +258,24 @@ int cda_host_free(cda_ctx* c, void* p) {
   CDA_API_CATCH(c)
 }
 
+int cda_host_register(cda_ctx* c, void* p, size_t bytes) {
+  CDA_API_TRY
+  if (!c || !p || !bytes) return CDA_E_ARG;
+  Lock l(c);
+  return dev_ok(c, hipHostRegister(p, bytes, hipHostRegisterDefault), "hipHostRegister") ? CDA_OK : CDA_E_DEVICE;
+  CDA_API_CATCH(c)
+}
+
+int cda_host_unregister(cda_ctx* c, void* p) {
+  CDA_API_TRY
+  if (!c || !p) return CDA_E_ARG;
+  Lock l(c);
+  // every DMA this context enqueued into or out of the range has finished before the pages are released
+  if (!dev_ok(c, hipStreamSynchronize(c->stream), "sync")) return CDA_E_DEVICE;
+  return dev_ok(c, hipHostUnregister(p), "hipHostUnregister") ? CDA_OK : CDA_E_DEVICE;
+  CDA_API_CATCH(c)
+}
+
 // ---- multi-device batch ----------------------------------------------------------------------
 // (struct cda_multi: ctx.h)
 

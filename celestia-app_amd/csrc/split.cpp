@@ -480,6 +480,24 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
   return map_status(st, -1, err);
 }
 
+// A failure on any device of the handle (an RCCL group call is issued per device; ncclCommInitAll reports into
+// device 0) is surfaced through cda_last_device_error(cda_multi_context(m, 0)): every device's message, each named
+// by its handle index and HIP device, with the RCCL error string.
+int split_call(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const* d_slabs, uint8_t* eds,
+               uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  for (auto* c : m->ctx) c->last_err.clear();
+  const int rc = split_impl(m, k, h_ods, d_slabs, eds, row_roots, col_roots, dah, err);
+  if (rc == CDA_E_DEVICE || rc == CDA_E_NOMEM || rc == CDA_E_INTERNAL) {
+    std::string all;
+    for (size_t g = 0; g < m->ctx.size(); g++)
+      if (!m->ctx[g]->last_err.empty())
+        all += (all.empty() ? "" : "; ") + std::string("split device ") + std::to_string(g) + " (HIP " +
+               std::to_string(m->ctx[g]->device) + "): " + m->ctx[g]->last_err;
+    m->ctx[0]->last_err = all.empty() ? std::string("split: device error (no detail recorded)") : all;
+  }
+  return rc;
+}
+
 int check_split_args(cda_multi* m, uint32_t k, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah) {
   if (!m || m->ctx.empty() || !row_roots || !col_roots || !dah) return CDA_E_ARG;
   if (!is_pow2(k)) return CDA_E_NOT_POW2;
@@ -524,7 +542,7 @@ int cda_multi_extend_commit_split(cda_multi* m, uint32_t k, const uint8_t* ods, 
   set_err(err, CDA_OK, -1, -1, -1, -1);
   if (!ods) return CDA_E_ARG;
   if (int rc = check_split_args(m, k, row_roots, col_roots, dah)) return rc;
-  return split_impl(m, k, ods, nullptr, eds_or_null, row_roots, col_roots, dah, err);
+  return split_call(m, k, ods, nullptr, eds_or_null, row_roots, col_roots, dah, err);
   CDA_API_CATCH(m && !m->ctx.empty() ? m->ctx[0] : nullptr)
 }
 
@@ -536,7 +554,7 @@ int cda_multi_extend_commit_split_device(cda_multi* m, uint32_t k, const void* c
   if (int rc = check_split_args(m, k, row_roots, col_roots, dah)) return rc;
   for (size_t g = 0; g < m->ctx.size(); g++)
     if (!d_ods_slabs[g]) return CDA_E_ARG;
-  return split_impl(m, k, nullptr, d_ods_slabs, nullptr, row_roots, col_roots, dah, err);
+  return split_call(m, k, nullptr, d_ods_slabs, nullptr, row_roots, col_roots, dah, err);
   CDA_API_CATCH(m && !m->ctx.empty() ? m->ctx[0] : nullptr)
 }
 

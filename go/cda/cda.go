@@ -146,6 +146,8 @@ func ptr(b []byte) *C.uint8_t {
 	return (*C.uint8_t)(unsafe.Pointer(&b[0]))
 }
 
+var errUnequal = errors.New("shares must all be the same length")
+
 // flatten copies equal-length shares into one contiguous buffer (what the C ABI takes).
 func flatten(shares [][]byte) ([]byte, int, error) {
 	if len(shares) == 0 {
@@ -153,11 +155,8 @@ func flatten(shares [][]byte) ([]byte, int, error) {
 	}
 	n := len(shares[0])
 	out := make([]byte, len(shares)*n)
-	for i, s := range shares {
-		if len(s) != n {
-			return nil, 0, errors.New("shares must all be the same length")
-		}
-		copy(out[i*n:], s)
+	if err := flattenInto(out, shares, n); err != nil {
+		return nil, 0, err
 	}
 	return out, n, nil
 }

@@ -10,6 +10,7 @@ import (
 	"bytes"
 	"crypto/sha256"
 	"math/rand"
+	"runtime"
 	"sort"
 	"testing"
 
@@ -129,6 +130,73 @@ func TestExtendSharesMatchesCPUPath(t *testing.T) {
 		require.Equal(t, wr, gr, "k=%d", k)
 		require.Equal(t, wc, gc, "k=%d", k)
 	}
+}
+
+// TestDataAvailabilityHeaderFromSharesMatchesCPUPath: the roots-only consensus entry (../patches/0004) equals
+// da.NewDataAvailabilityHeader(rsmt2d.ComputeExtendedDataSquare(...)) on the reference's CPU code, and fails where
+// it fails (not a power of two; a namespace-order violation).
+func TestDataAvailabilityHeaderFromSharesMatchesCPUPath(t *testing.T) {
+	r := rand.New(rand.NewSource(6))
+	for _, k := range []int{1, 2, 8, 32, 64, 128} {
+		s := sortedShares(r, k*k)
+		eds, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+		require.NoError(t, err)
+		want, err := da.NewDataAvailabilityHeader(eds)
+		require.NoError(t, err)
+		rows, cols, hash, err := cda.DataAvailabilityHeaderFromShares(s)
+		require.NoError(t, err)
+		require.Equal(t, want.RowRoots, rows, "k=%d", k)
+		require.Equal(t, want.ColumnRoots, cols, "k=%d", k)
+		require.Equal(t, want.Hash(), hash, "k=%d", k)
+		got, err := da.NewDataAvailabilityHeaderFromShares(s) // the pkg/da wrapper installed by extend_rocm.go
+		require.NoError(t, err)
+		require.Equal(t, want.Hash(), got.Hash(), "k=%d", k)
+	}
+	_, _, _, err := cda.DataAvailabilityHeaderFromShares(make([][]byte, 5))
+	require.Error(t, err)
+	s := sortedShares(r, 64)
+	s[3], s[40] = s[40], s[3]
+	_, _, _, err = cda.DataAvailabilityHeaderFromShares(s)
+	require.Error(t, err)
+}
+
+// TestEDSPoolRecycles: ExtendShares' squares live in pooled page-locked slabs; after the squares (and every slice of
+// their cells) are unreachable, a garbage collection returns the slabs, later squares reuse them, and every square
+// stays bit-exact however its slab came to it.
+func TestEDSPoolRecycles(t *testing.T) {
+	r := rand.New(rand.NewSource(7))
+	k := 64 // 8 MiB EDS: pooled
+	s := sortedShares(r, k*k)
+	ref, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+	require.NoError(t, err)
+	want := ref.Flattened()
+	seen := map[*byte]int{}
+	for i := 0; i < 12; i++ {
+		eds, err := cda.ExtendShares(s)
+		require.NoError(t, err)
+		flat := eds.Flattened()
+		require.Equal(t, want, flat, "call %d", i)
+		seen[&flat[0][0]]++
+		eds, flat = nil, nil
+		runtime.GC()
+		runtime.GC() // the finalizer of the slab runs after the first cycle finds it unreachable
+	}
+	require.Less(t, len(seen), 12, "no slab was reused")
+	// a square whose cells are still referenced keeps its slab: the next squares get other slabs
+	keep, err := cda.ExtendShares(s)
+	require.NoError(t, err)
+	cell := keep.GetCell(0, 0)
+	row0 := keep.Flattened()[0]
+	keep = nil
+	runtime.GC()
+	runtime.GC()
+	for i := 0; i < 4; i++ {
+		eds, err := cda.ExtendShares(sortedShares(r, k*k))
+		require.NoError(t, err)
+		_ = eds
+	}
+	require.Equal(t, cell, row0)
+	require.Equal(t, want[0], row0)
 }
 
 func TestExtendSquareSplitMatchesCPUPath(t *testing.T) {

@@ -34,18 +34,22 @@ func ExtendShares(s [][]byte) (*rsmt2d.ExtendedDataSquare, error) {
 	return ExtendSharesOn(mustDefault(), s)
 }
 
-// ExtendSharesOn is ExtendShares on a given context.
+// ExtendSharesOn is ExtendShares on a given context.  The shares are flattened into a pooled page-locked slab and
+// the EDS lands in a pooled page-locked slab that the returned square's cells live in (pool.go): both copies are
+// direct DMAs, the path csrc/consensus.cpp takes for pinned caller memory.
 func ExtendSharesOn(ctx *Context, s [][]byte) (*rsmt2d.ExtendedDataSquare, error) {
 	if !isPowerOfTwo(len(s)) {
 		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", len(s))
 	}
-	flat, n, err := flatten(s)
-	if err != nil {
+	n := len(s[0])
+	flat, arr := takeShares(ctx, len(s)*n)
+	defer giveShares(ctx, len(s)*n, arr)
+	if err := flattenInto(flat, s, n); err != nil {
 		return nil, err
 	}
 	k := squareSize(len(s))
 	w := 2 * k
-	eds := make([]byte, w*w*n)
+	eds := takeEDS(ctx, w*w*n)
 	rows := make([]byte, w*NodeSize)
 	cols := make([]byte, w*NodeSize)
 	dah := make([]byte, 32)
@@ -56,6 +60,40 @@ func ExtendSharesOn(ctx *Context, s [][]byte) (*rsmt2d.ExtendedDataSquare, error
 		return nil, toErr(rc, &info)
 	}
 	return importWithRoots(ctx, eds, w, n, rows, cols)
+}
+
+// DataAvailabilityHeaderFromShares is da.NewDataAvailabilityHeader(da.ExtendShares(s)) for callers that read only
+// the header -- PrepareProposal and ProcessProposal use nothing of the square but dah.Hash()
+// (app/prepare_proposal.go:65-93, app/process_proposal.go:137-151): the same row roots, column roots and data hash
+// (and the same errors: not a power of two, not a square, namespace push order) from one cda_extend_commit with no
+// EDS copied back.  pkg/da wraps it as da.NewDataAvailabilityHeaderFromShares (../patches/0004).
+func DataAvailabilityHeaderFromShares(s [][]byte) (rowRoots, colRoots [][]byte, dataHash []byte, err error) {
+	return DataAvailabilityHeaderFromSharesOn(mustDefault(), s)
+}
+
+// DataAvailabilityHeaderFromSharesOn is DataAvailabilityHeaderFromShares on a given context.
+func DataAvailabilityHeaderFromSharesOn(ctx *Context, s [][]byte) (rowRoots, colRoots [][]byte, dataHash []byte,
+	err error) {
+	if !isPowerOfTwo(len(s)) {
+		return nil, nil, nil, fmt.Errorf("number of shares is not a power of 2: got %d", len(s))
+	}
+	n := len(s[0])
+	flat, arr := takeShares(ctx, len(s)*n)
+	defer giveShares(ctx, len(s)*n, arr)
+	if err := flattenInto(flat, s, n); err != nil {
+		return nil, nil, nil, err
+	}
+	w := 2 * squareSize(len(s))
+	rows := make([]byte, w*NodeSize)
+	cols := make([]byte, w*NodeSize)
+	dah := make([]byte, 32)
+	var info C.cda_err_info
+	rc := C.cda_extend_commit(ctx.c, C.uint32_t(len(s)), C.uint32_t(n), ptr(flat), nil, ptr(rows), ptr(cols),
+		ptr(dah), &info)
+	if rc != 0 {
+		return nil, nil, nil, toErr(rc, &info)
+	}
+	return split(rows, w), split(cols, w), dah, nil
 }
 
 // importWithRoots wraps the GPU's EDS as an *rsmt2d.ExtendedDataSquare whose row and column roots are already

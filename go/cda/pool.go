@@ -1,0 +1,147 @@
+//go:build rocm
+
+package cda
+
+/*
+#include "cda.h"
+*/
+import "C"
+
+import (
+	"reflect"
+	"runtime"
+	"sync"
+	"unsafe"
+)
+
+// Page-locked host slabs for the one-block consensus path (csrc/consensus.cpp).
+//
+// PrepareProposal, ProcessProposal and ExtendBlock extend one square per call (app/prepare_proposal.go:65,
+// app/process_proposal.go:137, app/extend_block.go:25).  libcda moves a page-locked buffer by direct DMA, while a
+// fresh Go slice is pinned by the HIP runtime page by page on every call, and a never-touched one is first faulted in
+// by the kernel: the driver measured 1.05 ms per k=128 block with a fresh 32 MiB EDS slice per call against 0.66 ms
+// with page-locked buffers (BENCH_r04 host_buffers.one_block_fresh).  So the binding keeps two pools:
+//
+//   - share slabs: the flatten every call does anyway (the C ABI takes one contiguous ODS) goes into a registered
+//     slab that returns to its pool as soon as the call is over;
+//   - EDS slabs: the square ExtendShares returns is an *rsmt2d.ExtendedDataSquare whose cells are slices of the slab,
+//     so the slab may be reused only once nothing references any cell.  The slab is a Go heap object (an array from
+//     reflect.New) watched by a finalizer: the garbage collector runs it when the square and every slice of its
+//     cells are unreachable -- a caller that keeps eds.Flattened()'s cells keeps the slab alive -- and the finalizer
+//     puts the (still registered) slab back into the pool.
+//
+// The slabs are registered once with cda_host_register (hipHostRegister) and never freed while registered: the Go
+// heap does not move objects, and a pooled slab is referenced by the pool, so the pages the driver locked stay the
+// object's.  A pool that is full falls back to plain Go memory (the slower fresh-buffer path, same results).
+// Squares smaller than minPooled bytes are allocated plainly: their copies are short either way.
+const (
+	minPooled      = 1 << 20
+	maxLivePerSize = 4 // registered slabs per size (in use + free), per context
+)
+
+type slabKey struct {
+	ctx *Context
+	n   int
+}
+
+type bufferPool struct {
+	mu   sync.Mutex
+	free map[slabKey][]interface{} // each entry a *[n]byte from reflect.New, registered with ctx
+	live map[slabKey]int
+}
+
+var (
+	edsPool   = &bufferPool{free: map[slabKey][]interface{}{}, live: map[slabKey]int{}}
+	sharePool = &bufferPool{free: map[slabKey][]interface{}{}, live: map[slabKey]int{}}
+)
+
+func slabBytes(arr interface{}, n int) []byte {
+	return unsafe.Slice((*byte)(reflect.ValueOf(arr).UnsafePointer()), n)
+}
+
+// take returns a registered slab of n bytes (or plain memory when the pool is full / registration fails) and the
+// array object behind it (nil for plain memory).
+func (p *bufferPool) take(ctx *Context, n int) ([]byte, interface{}) {
+	if n < minPooled {
+		return make([]byte, n), nil
+	}
+	key := slabKey{ctx, n}
+	p.mu.Lock()
+	if l := p.free[key]; len(l) > 0 {
+		arr := l[len(l)-1]
+		p.free[key] = l[:len(l)-1]
+		p.mu.Unlock()
+		return slabBytes(arr, n), arr
+	}
+	if p.live[key] >= maxLivePerSize {
+		p.mu.Unlock()
+		return make([]byte, n), nil
+	}
+	p.live[key]++
+	p.mu.Unlock()
+	arr := reflect.New(reflect.ArrayOf(n, reflect.TypeOf(byte(0)))).Interface()
+	b := slabBytes(arr, n)
+	if rc := C.cda_host_register(ctx.c, unsafe.Pointer(&b[0]), C.size_t(n)); rc != 0 {
+		p.mu.Lock()
+		p.live[key]--
+		p.mu.Unlock()
+		return b, nil // plain (unregistered) memory: still correct, the slower path
+	}
+	return b, arr
+}
+
+// give puts a registered slab back (no-op for plain memory).
+func (p *bufferPool) give(ctx *Context, n int, arr interface{}) {
+	if arr == nil {
+		return
+	}
+	key := slabKey{ctx, n}
+	p.mu.Lock()
+	p.free[key] = append(p.free[key], arr)
+	p.mu.Unlock()
+}
+
+// takeEDS returns an EDS slab that goes back to the pool when the garbage collector finds it unreferenced.
+func takeEDS(ctx *Context, n int) []byte {
+	b, arr := edsPool.take(ctx, n)
+	if arr != nil {
+		runtime.SetFinalizer(arr, func(a interface{}) { edsPool.give(ctx, n, a) })
+	}
+	return b
+}
+
+// takeShares / giveShares bracket one call: the flattened ODS is dead once the C call has returned.
+func takeShares(ctx *Context, n int) ([]byte, interface{}) { return sharePool.take(ctx, n) }
+func giveShares(ctx *Context, n int, arr interface{})      { sharePool.give(ctx, n, arr) }
+
+// flattenInto copies equal-length shares into dst (len(shares) * share length bytes).
+func flattenInto(dst []byte, shares [][]byte, n int) error {
+	for i, s := range shares {
+		if len(s) != n {
+			return errUnequal
+		}
+		copy(dst[i*n:], s)
+	}
+	return nil
+}
+
+// Trim unregisters and drops every free slab of ctx (e.g. before closing a non-default context).  Slabs still
+// referenced by squares stay registered until they come back and are trimmed in a later call.
+func (x *Context) Trim() {
+	for _, p := range []*bufferPool{edsPool, sharePool} {
+		p.mu.Lock()
+		for key, l := range p.free {
+			if key.ctx != x {
+				continue
+			}
+			for _, arr := range l {
+				b := slabBytes(arr, key.n)
+				C.cda_host_unregister(x.c, unsafe.Pointer(&b[0]))
+				runtime.SetFinalizer(arr, nil)
+				p.live[key]--
+			}
+			delete(p.free, key)
+		}
+		p.mu.Unlock()
+	}
+}

@@ -76,6 +76,12 @@ const char* cda_last_device_error(cda_ctx* ctx);
 /* "release gfx950", or "diagnostic gfx950 <tags>" for a library built with a diagnostic define that changes what
  * the kernels compute (timing experiments only; no environment variable can do that to a release build). */
 const char* cda_build_info(void);
+/* Per-context options (default 0).  CDA_OPT_HUGE_PAGES = 1: when the one-block path gets a fresh, never-touched
+ * pageable EDS buffer, madvise(MADV_HUGEPAGE) its 2 MiB-aligned interior before faulting it in (faster first touch,
+ * but it changes the page policy of caller memory -- under cgo, Go heap; off unless asked for).  CDA_E_ARG for an
+ * unknown option. */
+enum { CDA_OPT_HUGE_PAGES = 1 };
+int cda_set_option(cda_ctx* ctx, int option, int64_t value);
 
 /* ---- rsmt2d.Codec (LeoRSCodec replacement) ---------------------------- */
 /* Replaces rsmt2d.LeoRSCodec selected by appconsts.DefaultCodec
@@ -118,6 +124,13 @@ int cda_extend_commit_batch(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const ui
 /* Pinned host memory for share / EDS buffers (hipHostMalloc); free with cda_host_free. */
 int cda_host_alloc(cda_ctx* ctx, size_t bytes, void** out);
 int cda_host_free(cda_ctx* ctx, void* p);
+/* Page-lock caller memory for reuse as share / EDS buffers (hipHostRegister): go/cda's buffer pools register Go-heap
+ * slabs once and recycle them through the garbage collector, so the consensus path's copies are direct DMAs
+ * (app/prepare_proposal.go:65, app/process_proposal.go:137, app/extend_block.go:25 through da.ExtendShares).
+ * Unregister only after the last call that used the range has returned (unregister waits for this context's
+ * stream first). */
+int cda_host_register(cda_ctx* ctx, void* p, size_t bytes);
+int cda_host_unregister(cda_ctx* ctx, void* p);
 
 /* ---- multi-device batch (SURVEY.md §8b "batch ... plus a device mask", §8e) ----
  * One handle over the GPUs in `device_mask` (bit d = HIP device d; 0 = all visible devices), one

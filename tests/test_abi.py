@@ -76,8 +76,10 @@ def test_new_entry_points_reject_null_context_without_gpu():
 def test_exception_barrier_without_gpu(monkeypatch):
     """No C++ exception crosses the C ABI (no abort; app/process_proposal.go:28-34 recovers Go panics
     only): an exception injected at entry (CDA_FAULT_INJECT=entry throws std::bad_alloc before the body runs) comes
-    back as CDA_E_NOMEM from every kind of entry point, not as std::terminate."""
-    L = cda.lib()
+    back as CDA_E_NOMEM from every kind of entry point, not as std::terminate.  Injection exists only in the
+    test-hooks build (libcda_hooks.so)."""
+    L = N.lib(N.HOOKS_LIB_PATH)
+    assert "test_hooks" in N.build_info(N.HOOKS_LIB_PATH)
     monkeypatch.setenv("CDA_FAULT_INJECT", "entry")
     assert L.cda_merkle_roots(None, 1, None, None, 90, None) == N.E_NOMEM
     assert L.cda_repair(None, 8, None, None, None, None, None) == N.E_NOMEM
@@ -87,3 +89,34 @@ def test_exception_barrier_without_gpu(monkeypatch):
     assert L.cda_merkle_roots(None, 1, None, None, 90, None) == N.E_ARG
     assert N.strerror(N.E_NOMEM) == "out of host memory"
     assert N.strerror(N.E_INTERNAL).startswith("internal error")
+
+
+def test_release_library_ignores_fault_injection(monkeypatch):
+    """the release libcda.so carries no test hook -- with CDA_FAULT_INJECT set at every site it still
+    runs its argument checks (CDA_E_ARG for a null context, not the injected CDA_E_NOMEM) and says it is a release
+    build.  The GPU side of this check (bit-exact results with the variable set) is tests/test_faults_gpu.py."""
+    L = cda.lib()
+    assert N.build_info() == "release gfx950"
+    for site in ("entry", "alloc", "thread"):
+        monkeypatch.setenv("CDA_FAULT_INJECT", site)
+        assert L.cda_merkle_roots(None, 1, None, None, 90, None) == N.E_ARG
+        assert L.cda_extend_commit(None, 4, 512, None, None, None, None, None, None) == N.E_ARG
+        assert L.cda_set_option(None, N.OPT_HUGE_PAGES, 1) == N.E_ARG
+        assert L.cda_host_register(None, None, 0) == N.E_ARG
+
+
+def test_release_library_reads_no_environment_per_call():
+    """the product path reads its A/B knobs once at cda_init (ctx fields), never per call -- no getenv
+    outside cda_init's knob block, a function-local static, the test hooks and the diagnostic builds' trace hooks."""
+    import glob
+    csrc = os.path.join(ROOT, "celestia-app_amd", "csrc")
+    for path in glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.hip")):
+        src = open(path).read()
+        for m in re.finditer(r"getenv\(", src):
+            line_start = src.rfind("\n", 0, m.start()) + 1
+            line = src[line_start:src.find("\n", m.start())]
+            ctx_before = src[max(0, m.start() - 1500):m.start()]
+            ok = ("static" in line or "static const" in ctx_before[-400:] or "cda_init" in ctx_before
+                  or "CDA_TEST_HOOKS" in ctx_before or "TRACE" in line or "find_local_cpus" in ctx_before
+                  or "CDA_NUMA_BIND" in line)
+            assert ok, f"{os.path.basename(path)}: per-call getenv: {line.strip()}"

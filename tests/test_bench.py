@@ -21,9 +21,20 @@ def _run_bench(*args):
     return json.loads(lines[0])
 
 
+def _check_ranks(r, n):
+    """The N > 1 line's self-verification: ranks_seen from an all_reduce over the run's group, one
+    report per rank (its own step time, host, pid), distinct ranks 0..n-1."""
+    rep = r["ranks"]
+    assert rep["ranks_seen"] == n and len(rep["per_rank"]) == n
+    assert sorted(p["rank"] for p in rep["per_rank"]) == list(range(n))
+    assert len({p["pid"] for p in rep["per_rank"]}) == n
+    assert [p["ms_per_step"] for p in sorted(rep["per_rank"], key=lambda p: p["rank"])] == [float(i) for i in range(n)]
+
+
 def test_bench_spawns_two_ranks():
     r = _run_bench("--gpus", "2", "--dry-run")
     assert r["n_gpus"] == 2 and r["ranks_seen"] == 2 and r["max_rank"] == 1
+    _check_ranks(r, 2)
     # config C5's split helper (started before the GPU is touched, run between two CPU barriers) answered
     assert r["k512_split"] == {"dry_run": True, "G": 2, "helper_wall_s": r["k512_split"]["helper_wall_s"]}
 
@@ -31,6 +42,7 @@ def test_bench_spawns_two_ranks():
 def test_bench_spawns_four_ranks():
     r = _run_bench("--gpus", "4", "--dry-run")
     assert r["n_gpus"] == 4 and r["ranks_seen"] == 4
+    _check_ranks(r, 4)
     assert r["k512_split"]["G"] == 4
 
 

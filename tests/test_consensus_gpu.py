@@ -52,23 +52,63 @@ def test_one_block_fresh_buffers(ctx, k, want_eds):
 
 @pytest.mark.parametrize("cons_in,cons_out", [("1", "0"), ("2", "0"), ("1", "2"), ("2", "2")])
 @pytest.mark.parametrize("stg", [None, "0", "3"])
-@pytest.mark.parametrize("k", [16, 128])
-@pytest.mark.parametrize("buf", ["fresh", "written"])
-def test_one_block_forms(ctx, monkeypatch, cons_in, cons_out, stg, k, buf):
+@pytest.mark.parametrize("huge", [None, "1"])
+def test_one_block_forms(monkeypatch, cons_in, cons_out, stg, huge):
     """Every input form (CDA_CONS_IN: four bands / one copy) with every pageable output form (CDA_CONS_OUT=0: chosen
     by residency -- fresh buffers are touched by the pool and sent in pieces; 2: the written-buffer form forced, so
-    the runtime faults a fresh buffer in itself) and bottom-half split (CDA_CONS_STG: default half staged through the
-    pinned slab, 0 = all pageable, 3 MiB), fresh and written output buffers."""
+    the runtime faults a fresh buffer in itself), bottom-half split (CDA_CONS_STG: default half staged through the
+    pinned slab, 0 = all pageable, 3 MiB) and the opt-in huge-page hint (CDA_HUGE_PAGES), fresh and written output
+    buffers, k = 16 and 128.  The knobs are read once at cda_init, so each form gets its own context."""
+    import cda
     monkeypatch.setenv("CDA_CONS_IN", cons_in)
     monkeypatch.setenv("CDA_CONS_OUT", cons_out)
     if stg is not None:
         monkeypatch.setenv("CDA_CONS_STG", stg)
-    ods = O.gen_ods(k, 0xF0F0 + k)
-    out = np.empty((1, 4 * k * k, 512), np.uint8) if buf == "fresh" else np.full((1, 4 * k * k, 512), 0x3C, np.uint8)
-    eds, rr, cr, dah = ctx.extend_commit_batch(ods[None].copy(), eds_out=out)
-    _check(ods, out[0], rr[0], cr[0], dah[0])
-    _, rr2, cr2, dah2 = ctx.extend_commit_batch(ods[None].copy(), want_eds=False)
-    assert np.array_equal(rr2, rr) and np.array_equal(cr2, cr) and bytes(dah2[0]) == bytes(dah[0])
+    if huge is not None:
+        monkeypatch.setenv("CDA_HUGE_PAGES", huge)
+    c = cda.Context(0)
+    try:
+        for k in (16, 128):
+            ods = O.gen_ods(k, 0xF0F0 + k)
+            for buf in ("fresh", "written"):
+                out = (np.empty((1, 4 * k * k, 512), np.uint8) if buf == "fresh"
+                       else np.full((1, 4 * k * k, 512), 0x3C, np.uint8))
+                eds, rr, cr, dah = c.extend_commit_batch(ods[None].copy(), eds_out=out)
+                _check(ods, out[0], rr[0], cr[0], dah[0])
+                _, rr2, cr2, dah2 = c.extend_commit_batch(ods[None].copy(), want_eds=False)
+                assert np.array_equal(rr2, rr) and np.array_equal(cr2, cr) and bytes(dah2[0]) == bytes(dah[0])
+    finally:
+        c.close()
+
+
+def test_one_block_registered_caller_buffers(ctx):
+    """Caller memory page-locked once with cda_host_register and reused (go/cda's buffer pools): the shares and the
+    EDS buffer take the direct DMA path, several calls in a row, every result exact; unregistered afterwards."""
+    k = 128
+    ods_buf = np.empty((1, k * k, 512), np.uint8)
+    eds_buf = np.full((1, 4 * k * k, 512), 0x77, np.uint8)
+    ctx.host_register(ods_buf)
+    ctx.host_register(eds_buf)
+    try:
+        for seed in (0x301, 0x302, 0x303):
+            ods = O.gen_ods(k, seed)
+            ods_buf[0] = ods
+            _, rr, cr, dah = ctx.extend_commit_batch(ods_buf, eds_out=eds_buf)
+            _check(ods, eds_buf[0], rr[0], cr[0], dah[0])
+            _, rr2, cr2, dah2 = ctx.extend_commit_batch(ods_buf, want_eds=False)
+            assert bytes(dah2[0]) == bytes(dah[0])
+    finally:
+        ctx.host_unregister(ods_buf)
+        ctx.host_unregister(eds_buf)
+
+
+def test_set_option_validates(ctx):
+    import cda
+    from cda import _native as N
+    ctx.set_option(N.OPT_HUGE_PAGES, 1)
+    ctx.set_option(N.OPT_HUGE_PAGES, 0)
+    with pytest.raises(cda.CdaError):
+        ctx.set_option(12345, 1)
 
 
 @pytest.mark.parametrize("k", [64, 128])
@@ -168,7 +208,7 @@ def test_one_block_copy_pool_fault_is_a_return_code(monkeypatch):
     """The copy pool's threads cannot start: CDA_E_INTERNAL, and the next call on the context works."""
     import cda
     from cda import _native as N
-    c = cda.Context(0)
+    c = cda.Context(0, lib_path=N.HOOKS_LIB_PATH)  # failure injection: the test-hooks build only
     try:
         ods = O.gen_ods(32, 9)
         monkeypatch.setenv("CDA_FAULT_INJECT", "thread")

@@ -173,6 +173,37 @@ def test_batched_and_per_tx_agree():
         P.validate_blob_tx(t, precomputed=None, ctx=eng)
 
 
+class RecordingCommitments(OracleCommitments):
+    """Records the namespaces of every blob handed to the batch call."""
+
+    def __init__(self):
+        super().__init__()
+        self.batches = []
+
+    def blob_commitments(self, namespaces, datas, share_versions=None, subtree_root_threshold=64):
+        self.batches.append([bytes(n) for n in namespaces])
+        return super().blob_commitments(namespaces, datas, share_versions, subtree_root_threshold)
+
+
+@pytest.mark.parametrize("which", ["reserved", "zero"])
+def test_blob_tx_rejected_by_validate_blobs_is_left_out_of_the_batch(which):
+    """the batch holds exactly the BlobTxs whose blobs ValidateBlobs accepts (the Go pre-pass's filter):
+    a reserved-namespace blob (and an empty one) stays out of the batched call, is checked on its own, and is reported
+    at its index with the reference's error."""
+    txs = random_proposal(21)
+    bad, code = _tamper(22, which)
+    txs.insert(3, bad)
+    _, bad_blobs = S.unmarshal_blob_tx(bad)
+    eng = RecordingCommitments()
+    pre = P.precompute_commitments(txs, ctx=eng)
+    assert pre[3] is None and eng.calls == 1
+    assert all(bytes(b["ns"]) not in eng.batches[0] for b in bad_blobs) or which == "zero"
+    n_good_blobs = sum(len(S.unmarshal_blob_tx(t)[1]) for i, t in enumerate(txs)
+                       if i != 3 and S.unmarshal_blob_tx(t) is not None)
+    assert len(eng.batches[0]) == n_good_blobs
+    assert P.process_proposal_blob_txs(txs, ctx=RecordingCommitments()) == (3, code)
+
+
 def test_namespace_rules():
     assert P.namespace_error(bytes(29)) == "ErrReservedNamespace"
     assert P.namespace_error(bytes(28) + b"\xff") == "ErrReservedNamespace"
