@@ -321,3 +321,53 @@ def device_plan(segs):
         data.append(payload)
         off += len(payload)
     return recs, np.frombuffer(b"".join(data) or b"\0", np.uint8), np.array(reserved or [0], np.uint32)
+
+
+def segments_from_shares(shares):
+    """The layout plan read back from a constructed square's shares (go/cda/square.go SegmentsFromShares, its Go
+    twin): ns ‖ info (share version << 1 | sequence start) ‖ sequence length (first share) ‖ reserved bytes (compact
+    shares) ‖ payload.  A run of identical shares of sequence length 0 outside the compact namespaces is padding.
+    Returns device_plan's triple (cda_share_segment records, payload bytes, reserved values), so only the payload
+    crosses PCIe in cda_construct_extend_commit."""
+    import numpy as np
+    from ._native import ShareSegment
+    segs, data, reserved, off, i = [], [], [], 0, 0
+    while i < len(shares):
+        sh = bytes(shares[i])
+        if len(sh) != SHARE:
+            raise SquareError(f"share {i} is {len(sh)} bytes")
+        ns, info = sh[:NS], sh[NS]
+        if not info & 1:
+            raise SquareError(f"share {i} continues no sequence")
+        seq_len = int.from_bytes(sh[NS + 1:NS + 5], "big")
+        compact = ns in (TX_NAMESPACE, PAY_FOR_BLOB_NAMESPACE)
+        if not compact and seq_len == 0:
+            j = i + 1
+            while j < len(shares) and bytes(shares[j]) == sh:
+                j += 1
+            segs.append(dict(kind=SEG_KIND["padding"], first=i, n=j - i, version=info >> 1, ns=ns, off=off, len=0,
+                             roff=0))
+            i = j
+            continue
+        hdr0, hdrn = (NS + 9, NS + 5) if compact else (NS + 5, NS + 1)
+        payload, resv, j = bytearray(), [], i
+        while j < len(shares) and (j == i or (bytes(shares[j][:NS]) == ns and not shares[j][NS] & 1)):
+            h = hdr0 if j == i else hdrn
+            if compact:
+                resv.append(int.from_bytes(bytes(shares[j][h - 4:h]), "big"))
+            payload += bytes(shares[j][h:])
+            j += 1
+        if len(payload) < seq_len:
+            raise SquareError(f"sequence at share {i} is shorter than its length {seq_len}")
+        segs.append(dict(kind=SEG_KIND["compact" if compact else "sparse"], first=i, n=j - i, version=info >> 1,
+                         ns=ns, off=off, len=seq_len, roff=len(reserved) if compact else 0))
+        data.append(bytes(payload[:seq_len]))
+        reserved += resv
+        off += seq_len
+        i = j
+    recs = (ShareSegment * len(segs))()
+    for r, sg in zip(recs, segs):
+        r.kind, r.first_share, r.nshares, r.share_version = sg["kind"], sg["first"], sg["n"], sg["version"]
+        r.data_off, r.data_len, r.reserved_off = sg["off"], sg["len"], sg["roff"]
+        r.ns[:] = list(sg["ns"])
+    return recs, np.frombuffer(b"".join(data) or b"\0", np.uint8), np.array(reserved or [0], np.uint32)

@@ -5,11 +5,20 @@
  * include/cda.h); run by tests/test_abi_client.py on the GPU, which checks its outputs against
  * tests/golden/oracle_digests.json and mainnet block 408's data_hash.
  *
- *   abi_host_client <ods.bin> <k> <out_dir> [<blobs.bin>]
+ *   abi_host_client <ods.bin> <k> <out_dir> [<blobs.bin>] [--proof <start> <end>] [--nodes] [--segments <segs.bin>]
  * writes <out_dir>/{eds,row_roots,col_roots,dah,parity,repaired,commitments}.bin and prints one status line.
  * With <blobs.bin> ([u32 n][n x 29-B namespace][(n + 1) x u64 data offsets][data]) it also computes the share
  * commitments of all n blobs in ONE cda_blob_commitments call -- ProcessProposal's pre-pass over every BlobTx of a
  * proposal (go/patches/0003) -- into <out_dir>/proposal_commitments.bin.
+ * The calls go/cda's f1 / f3 bindings make (go/cda/proof.go, go/cda/square.go; go/patches/0005):
+ *   --proof S E   pkg/proof NewShareInclusionProof of ODS shares [S, E) (cda_share_inclusion_proof) -> proof.bin:
+ *                 cda_share_proof_info | row roots | leaf hashes | aunts | nmt start, end, count (i32) | nmt nodes |
+ *                 data root, each section sized by the info (capacity k rows);
+ *   --nodes       pkg/inclusion's subtree cacher: every node of every row / column tree and of the DAH tree
+ *                 (cda_extend_commit_nodes) -> row_nodes.bin, col_nodes.bin, dah_nodes.bin;
+ *   --segments F  square.Construct on the device from a host layout plan (cda_construct_extend_commit); F =
+ *                 [u32 nseg][nseg x cda_share_segment][u64 data_len][data][u32 nres][nres x u32] ->
+ *                 construct_ods.bin, construct_dah.bin.
  * Also checked in-process: Codec.Decode of an erased row, a wrapper tree root, the multi-device batch.
  */
 #include <stdint.h>
@@ -35,9 +44,142 @@ static int fail(const char* what, int rc, const cda_err_info* e) {
   return 1;
 }
 
+static uint8_t* read_all(const char* path, size_t* n) {
+  FILE* f = fopen(path, "rb");
+  if (!f || fseek(f, 0, SEEK_END) != 0) return NULL;
+  const long sz = ftell(f);
+  uint8_t* b = malloc((size_t)sz + 1);
+  rewind(f);
+  if (sz < 0 || fread(b, 1, (size_t)sz, f) != (size_t)sz) {
+    fclose(f);
+    free(b);
+    return NULL;
+  }
+  fclose(f);
+  *n = (size_t)sz;
+  return b;
+}
+
+/* pkg/proof NewShareInclusionProof through cda_share_inclusion_proof (what go/cda.ShareInclusionProof binds) */
+static int run_proof(cda_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t start, uint32_t end, const char* dir) {
+  const uint32_t lg = (uint32_t)__builtin_ctz(2 * k), cap = k, naunts_max = lg + 1, max_nodes = 2 * lg;
+  cda_share_proof_info info;
+  uint8_t* rr = malloc((size_t)cap * CDA_NODE_SIZE);
+  uint8_t* lh = malloc((size_t)cap * 32);
+  uint8_t* au = malloc((size_t)cap * naunts_max * 32);
+  int32_t* ns = malloc((size_t)cap * 4 * 3);
+  uint8_t* nodes = malloc((size_t)cap * (max_nodes ? max_nodes : 1) * CDA_NODE_SIZE);
+  uint8_t root[32];
+  cda_err_info err;
+  int rc = cda_share_inclusion_proof(ctx, k * k, CDA_SHARE_SIZE, ods, start, end, &info, rr, lh, au, ns, ns + cap,
+                                     ns + 2 * cap, nodes, root, &err);
+  if (rc) return fail("cda_share_inclusion_proof", rc, &err);
+  char path[4096];
+  snprintf(path, sizeof path, "%s/proof.bin", dir);
+  FILE* f = fopen(path, "wb");
+  if (!f) return 1;
+  fwrite(&info, sizeof info, 1, f);
+  fwrite(rr, CDA_NODE_SIZE, info.nrows, f);
+  fwrite(lh, 32, info.nrows, f);
+  for (uint32_t i = 0; i < info.nrows; i++) fwrite(au + (size_t)i * naunts_max * 32, 32, info.naunts, f);
+  fwrite(ns, 4, info.nrows, f);
+  fwrite(ns + cap, 4, info.nrows, f);
+  fwrite(ns + 2 * cap, 4, info.nrows, f);
+  for (uint32_t i = 0; i < info.nrows; i++)
+    fwrite(nodes + (size_t)i * info.max_nodes * CDA_NODE_SIZE, CDA_NODE_SIZE, (size_t)ns[2 * cap + i], f);
+  fwrite(root, 32, 1, f);
+  fclose(f);
+  free(rr), free(lh), free(au), free(ns), free(nodes);
+  return 0;
+}
+
+/* every tree node the block path builds (cda_extend_commit_nodes; go/cda.ExtendCommitNodes) */
+static int run_nodes(cda_ctx* ctx, const uint8_t* ods, uint32_t k, const uint8_t* dah_want, const char* dir) {
+  const uint32_t w = 2 * k;
+  const size_t tree_b = (size_t)w * (2 * w - 1) * CDA_NODE_SIZE;
+  uint8_t* rn = malloc(tree_b);
+  uint8_t* cn = malloc(tree_b);
+  uint8_t* dn = malloc((size_t)(4 * w - 1) * 32);
+  uint8_t* rows = malloc((size_t)w * CDA_NODE_SIZE);
+  uint8_t* cols = malloc((size_t)w * CDA_NODE_SIZE);
+  uint8_t dah[32];
+  cda_err_info err;
+  int rc = cda_extend_commit_nodes(ctx, k * k, CDA_SHARE_SIZE, ods, NULL, rows, cols, dah, rn, cn, dn, &err);
+  if (rc) return fail("cda_extend_commit_nodes", rc, &err);
+  if (memcmp(dah, dah_want, 32) != 0 || memcmp(dn + (size_t)(4 * w - 2) * 32, dah, 32) != 0) {
+    fprintf(stderr, "node export DAH differs\n");
+    return 1;
+  }
+  for (uint32_t t = 0; t < w; t++)  /* each tree's last node is its root */
+    if (memcmp(rn + ((size_t)t * (2 * w - 1) + 2 * w - 2) * CDA_NODE_SIZE, rows + (size_t)t * CDA_NODE_SIZE, CDA_NODE_SIZE) ||
+        memcmp(cn + ((size_t)t * (2 * w - 1) + 2 * w - 2) * CDA_NODE_SIZE, cols + (size_t)t * CDA_NODE_SIZE, CDA_NODE_SIZE)) {
+      fprintf(stderr, "exported root of tree %u differs\n", t);
+      return 1;
+    }
+  if (write_file(dir, "row_nodes.bin", rn, tree_b) || write_file(dir, "col_nodes.bin", cn, tree_b) ||
+      write_file(dir, "dah_nodes.bin", dn, (size_t)(4 * w - 1) * 32))
+    return 1;
+  free(rn), free(cn), free(dn), free(rows), free(cols);
+  return 0;
+}
+
+/* square.Construct + ExtendShares + NewDataAvailabilityHeader from a layout plan (cda_construct_extend_commit;
+ * go/cda.ConstructExtendCommit) */
+static int run_segments(cda_ctx* ctx, uint32_t k, const char* path, const char* dir) {
+  size_t n = 0;
+  uint8_t* b = read_all(path, &n);
+  if (!b || n < 4) return 2;
+  uint32_t nseg;
+  memcpy(&nseg, b, 4);
+  const cda_share_segment* segs = (const cda_share_segment*)(b + 4);
+  size_t at = 4 + (size_t)nseg * sizeof(cda_share_segment);
+  uint64_t dlen;
+  memcpy(&dlen, b + at, 8);
+  const uint8_t* data = b + at + 8;
+  at += 8 + dlen;
+  uint32_t nres;
+  memcpy(&nres, b + at, 4);
+  uint32_t* res = malloc(((size_t)nres + 1) * 4);
+  memcpy(res, b + at + 4, (size_t)nres * 4);
+  const uint32_t w = 2 * k;
+  uint8_t* ods = malloc((size_t)k * k * CDA_SHARE_SIZE);
+  uint8_t* rows = malloc((size_t)w * CDA_NODE_SIZE);
+  uint8_t* cols = malloc((size_t)w * CDA_NODE_SIZE);
+  uint8_t dah[32];
+  cda_err_info err;
+  int rc = cda_construct_extend_commit(ctx, k, nseg, segs, data, dlen, res, nres, ods, NULL, rows, cols, dah, &err);
+  if (rc) return fail("cda_construct_extend_commit", rc, &err);
+  if (write_file(dir, "construct_ods.bin", ods, (size_t)k * k * CDA_SHARE_SIZE) ||
+      write_file(dir, "construct_dah.bin", dah, 32))
+    return 1;
+  free(b), free(res), free(ods), free(rows), free(cols);
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  if (argc != 4 && argc != 5) {
-    fprintf(stderr, "usage: %s <ods.bin> <k> <out_dir> [<blobs.bin>]\n", argv[0]);
+  const char* blobs_path = NULL;
+  const char* segs_path = NULL;
+  int want_nodes = 0, want_proof = 0;
+  uint32_t p_start = 0, p_end = 0;
+  for (int a = 4; a < argc; a++) {
+    if (!strcmp(argv[a], "--proof") && a + 2 < argc) {
+      want_proof = 1;
+      p_start = (uint32_t)atoi(argv[++a]);
+      p_end = (uint32_t)atoi(argv[++a]);
+    } else if (!strcmp(argv[a], "--nodes")) {
+      want_nodes = 1;
+    } else if (!strcmp(argv[a], "--segments") && a + 1 < argc) {
+      segs_path = argv[++a];
+    } else if (a == 4 && strncmp(argv[a], "--", 2) != 0) {
+      blobs_path = argv[a];
+    } else {
+      argc = 0;
+      break;
+    }
+  }
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s <ods.bin> <k> <out_dir> [<blobs.bin>] [--proof S E] [--nodes] [--segments F]\n",
+            argv[0]);
     return 2;
   }
   const uint32_t k = (uint32_t)atoi(argv[2]), w = 2 * k, count = k * k;
@@ -137,17 +279,17 @@ int main(int argc, char** argv) {
   if (rc) return fail("cda_blob_commitments", rc, &err);
 
   /* ProcessProposal's pre-pass: every blob of a proposal in one call */
-  if (argc == 5) {
-    FILE* bf = fopen(argv[4], "rb");
+  if (blobs_path) {
+    FILE* bf = fopen(blobs_path, "rb");
     if (!bf || fseek(bf, 0, SEEK_END) != 0) {
-      fprintf(stderr, "cannot read %s\n", argv[4]);
+      fprintf(stderr, "cannot read %s\n", blobs_path);
       return 2;
     }
     const long bsz = ftell(bf);
     uint8_t* bb = malloc((size_t)bsz + 1);
     rewind(bf);
     if (bsz < 4 || fread(bb, 1, (size_t)bsz, bf) != (size_t)bsz) {
-      fprintf(stderr, "cannot read %s\n", argv[4]);
+      fprintf(stderr, "cannot read %s\n", blobs_path);
       return 2;
     }
     fclose(bf);
@@ -186,6 +328,10 @@ int main(int argc, char** argv) {
     return 1;
   }
   cda_multi_free(multi);
+
+  if (want_proof && (rc = run_proof(ctx, ods, k, p_start, p_end, argv[3]))) return rc;
+  if (want_nodes && (rc = run_nodes(ctx, ods, k, dah, argv[3]))) return rc;
+  if (segs_path && (rc = run_segments(ctx, k, segs_path, argv[3]))) return rc;
 
   if (write_file(argv[3], "commitments.bin", commitments, sizeof commitments) ||
       write_file(argv[3], "eds.bin", eds, (size_t)w * w * S) || write_file(argv[3], "row_roots.bin", rows, (size_t)w * CDA_NODE_SIZE) ||

@@ -116,3 +116,24 @@ def test_device_square_matches_host(ctx, seed, n_normal, n_blob):
     assert np.array_equal(ods, host)
     rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(host)
     assert rc == 0 and dah == dah_o and np.array_equal(eds, eds_o)
+
+
+def _recs_tuple(recs):
+    return [(r.kind, r.first_share, r.nshares, r.share_version, r.data_off, r.data_len, r.reserved_off, bytes(r.ns))
+            for r in recs]
+
+
+@pytest.mark.parametrize("seed,n_normal,n_blob", [(408, None, None), (1, 40, 0), (2, 0, 6), (3, 25, 12)])
+def test_segments_from_shares_reads_back_the_plan(seed, n_normal, n_blob):
+    """go/cda SegmentsFromShares (mirrored by cda.square.segments_from_shares): reading the layout back from a
+    constructed square gives exactly the planner's device plan -- records, payload and reserved bytes -- for mainnet
+    block 408 and synthetic blocks of normal txs and multi-blob BlobTxs."""
+    if seed == 408:
+        txs, _ = mainnet_txs()
+    else:
+        txs = _random_txs(seed, n_normal, n_blob)
+    ss, segs, _ = S.plan(txs, 128, 64)
+    want = S.device_plan(segs)
+    got = S.segments_from_shares(S.render(segs))
+    assert _recs_tuple(got[0]) == _recs_tuple(want[0])
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
