@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-5 GPU runs: each argument names a stage, run in order; every GPU step under its own time limit, the script
+# stops at the first failure.  Outputs under gpurun_out/r05<tag>_*.
+#   tests        the whole -m gpu suite
+#   consensus    scripts/consensus_shapes.py (the one-block call in every go/cda shape), 3 rounds
+#   rs16ab       GF(2^16) encoder probe, release vs ab/libcda_touch0.so, 3 rotations
+#   bench        bench.py (default: N = 1, full extras + CPU baseline)
+#   profile      scripts/profile.sh r05 (rocprofv3 kernel trace + PMC passes of bench.py --steps 5)
+set -u
+TAG=${TAG:-a}
+mkdir -p gpurun_out
+O=gpurun_out/r05${TAG}
+for stage in "$@"; do
+  case $stage in
+    tests)
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > ${O}_tests.log 2>&1
+      rc=$?; tail -n 3 ${O}_tests.log; [ $rc -ne 0 ] && exit $rc ;;
+    consensus)
+      timeout -k 10 400 python -u scripts/consensus_shapes.py 25 3 > ${O}_shapes.log 2>&1
+      rc=$?; tail -c 2500 ${O}_shapes.log; [ $rc -ne 0 ] && exit $rc ;;
+    rs16ab)
+      for i in 1 2 3; do
+        for lib in celestia-app_amd/cda/libcda.so ab/libcda_touch0.so; do
+          echo "$lib $(CDA_LIB=$lib timeout -k 10 120 python scripts/rs16_probe.py 20)" >> ${O}_rs16ab.log || exit 1
+        done
+      done
+      cat ${O}_rs16ab.log ;;
+    bench)
+      timeout -k 10 900 python -u bench.py > ${O}_bench.log 2>&1
+      rc=$?; tail -c 1500 ${O}_bench.log; [ $rc -ne 0 ] && exit $rc ;;
+    profile)
+      timeout -k 10 900 bash scripts/profile.sh r05${TAG} > ${O}_profile.log 2>&1
+      rc=$?; tail -n 20 ${O}_profile.log; [ $rc -ne 0 ] && exit $rc ;;
+    *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done
