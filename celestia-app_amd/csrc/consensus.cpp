@@ -11,7 +11,8 @@
 //   ODS    : up band by band, each band's RS row pass launched as soon as its copy lands.
 //   Q0     : the EDS's top-left quadrant IS the ODS (rsmt2d copies the shares in): the pool copies it host to host
 //            from the caller's ODS into the caller's EDS -- it never crosses PCIe.
-//   Q1     : each band's right halves come back (one 2-D DMA per band) right after that band's row pass.
+//   Q1     : each band's right halves come back into a pinned slab (one DMA per band) right after that band's row pass,
+//            and the pool copies them into the caller's rows.
 //   Q2|Q3  : the bottom half comes back right after the column pass, while the leaf hashing, the trees and the DAH
 //            run on the compute stream.
 //   pages  : a fresh output gets transparent huge pages and is touched by the pool while the device works.
@@ -290,10 +291,13 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // 0.447 vs 0.452 ms roots only and was slower with the EDS (r04_pass8.log): the rows pass of one block is
 // latency-bound (~20 us whatever its size), so the device chain after the input is the same either way.
 // Output, by what the caller's EDS buffer is:
-//   pinned      Q1 and the bottom half straight to it by DMA;
-//   resident    Q1 through the pinned slab (copy pool), the bottom half split between a pageable DMA (the written
-//               pages pin cheaply) and the pinned slab (below);
-//   fresh       huge pages asked for and every page first touched by the pool (one 2 MiB range per task) while the
+//   (every form: Q1 through the pinned slab, copied into the caller's rows by the pool -- a strided D2H runs at half
+//   the link rate)
+//   pinned      the bottom half straight to it by one DMA;
+//   resident    the bottom half split between a pageable DMA (the written pages pin cheaply) and the pinned slab
+//               (below);
+//   fresh       huge pages asked for (only if the caller opted in) and every page first touched by the pool (one 2 MiB
+//               range per task) while the
 //               device works, then the resident form, the pageable part of the bottom half in pieces, each sent once
 //               its pages are touched.  A pageable DMA into never-touched memory faults it page by page in one thread (3.6 ms
 //               per block, r04_pass1); sending the bottom half through the pinned slab in 1 MiB chunks copied out by
@@ -337,7 +341,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const size_t stg_b = (want && !out_pinned) ? std::min(bot_b / 4 * 3, stg_want / (2 * erowS) * (2 * erowS)) : 0;
   const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
   const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
-  if ((want && !out_pinned && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
+  if ((want && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
       (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
     return rc;
   if (fresh && c->huge_pages) want_huge_pages(eds_or_null, eds_b);  // opt-in only (cda_set_option)
@@ -382,8 +386,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
           }
         });
       }
-    if (!out_pinned)
-      for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its 2-D DMA has landed
+    for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its DMA into the slab has landed
         for (uint32_t r0 = b * kb; r0 < (b + 1) * kb; r0 += rows_per_task)
           tasks.emplace_back([=, &q1_rec, &abort] {
             if (!wait_count(q1_rec, (int)b + 1, abort) || !wait_event(X->ev_q1[b], abort)) return;
@@ -445,8 +448,12 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       break;
     }
     if (want) {
-      uint8_t* dst = out_pinned ? eds_or_null + r0 * erowS + rowS : X->pin_out + r0 * rowS;
-      const size_t dpitch = out_pinned ? erowS : rowS;
+      // Q1 lands contiguously in the pinned slab whatever the caller's buffer is: a DMA into the strided right halves
+      // of the caller's rows ran at half the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, whether the
+      // caller's memory is pinned or not; a strided DEVICE source costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py,
+      // profiles/r05_pcie_duplex.log), so the pool moves the rows into place host to host.
+      uint8_t* dst = X->pin_out + r0 * rowS;
+      const size_t dpitch = rowS;
       if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
           hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
           hipMemcpy2DAsync(dst, dpitch, d_eds + r0 * erowS + rowS, erowS, rowS, kb, hipMemcpyDeviceToHost,

@@ -706,6 +706,26 @@ __device__ __forceinline__ void touch_round(const Args& a, int g_next, uint32_t 
 }
 #pragma clang diagnostic pop
 
+// Parity stores of the persistent loop.  CDA_RS16_NT_STORES=1 (A/B builds) marks them non-temporal: the bottom half
+// is read next by the leaf hashing, not by this kernel, so keeping it out of L2 could let the next round's cached
+// input stay there.
+#ifndef CDA_RS16_NT_STORES
+#define CDA_RS16_NT_STORES 0
+#endif
+__device__ __forceinline__ void store_parity(uint4* o, const uint4& q0, const uint4& q1, const uint4& q2,
+                                             const uint4& q3) {
+#if CDA_RS16_NT_STORES
+  typedef unsigned v4 __attribute__((ext_vector_type(4)));
+  v4* p = reinterpret_cast<v4*>(o);
+  __builtin_nontemporal_store(v4{q0.x, q0.y, q0.z, q0.w}, p);
+  __builtin_nontemporal_store(v4{q1.x, q1.y, q1.z, q1.w}, p + 8);
+  __builtin_nontemporal_store(v4{q2.x, q2.y, q2.z, q2.w}, p + 16);
+  __builtin_nontemporal_store(v4{q3.x, q3.y, q3.z, q3.w}, p + 24);
+#else
+  o[0] = q0, o[8] = q1, o[16] = q2, o[24] = q3;
+#endif
+}
+
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 u4(v4u v) { return make_uint4(v.x, v.y, v.z, v.w); }
 template <int N>
@@ -878,7 +898,7 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
         uint4 q0, q1, q2, q3;
         from_state(E[r], m1, ko, q0, q1, q2, q3);
         uint4* o = reinterpret_cast<uint4*>(dst + (pl + pos_r(LA, r)) * a.dst_sh);
-        o[0] = q0, o[8] = q1, o[16] = q2, o[24] = q3;
+        store_parity(o, q0, q1, q2, q3);
         if (r >= 2) {
           const uint4* p = reinterpret_cast<const uint4*>(srcn + (pl + pos_r(LA, r)) * shn);
           R[r - 2][0] = p[0], R[r - 2][1] = p[8], R[r - 2][2] = p[16], R[r - 2][3] = p[24];

@@ -3,7 +3,9 @@
 # stops at the first failure.  Outputs under gpurun_out/r05<tag>_*.
 #   tests        the whole -m gpu suite
 #   consensus    scripts/consensus_shapes.py (the one-block call in every go/cda shape), 3 rounds
-#   rs16ab       GF(2^16) encoder probe, release vs ab/libcda_touch0.so, 3 rotations
+#   rs16ab       GF(2^16) encoder probe over the libraries in $LIBS (default: release, ab/libcda_touch0.so,
+#                ab/libcda_nt.so), 3 rotations
+#   constrace    scripts/consensus_trace.py (phase trace of the page-locked one-block path, after a D2H warm-up)
 #   bench        bench.py (default: N = 1, full extras + CPU baseline)
 #   profile      scripts/profile.sh r05 (rocprofv3 kernel trace + PMC passes of bench.py --steps 5)
 set -u
@@ -18,9 +20,15 @@ for stage in "$@"; do
     consensus)
       timeout -k 10 400 python -u scripts/consensus_shapes.py 25 3 > ${O}_shapes.log 2>&1
       rc=$?; tail -c 2500 ${O}_shapes.log; [ $rc -ne 0 ] && exit $rc ;;
+    duplex)
+      timeout -k 10 120 python -u scripts/pcie_duplex_probe.py > ${O}_duplex.log 2>&1
+      rc=$?; tail -c 1000 ${O}_duplex.log; [ $rc -ne 0 ] && exit $rc ;;
+    constrace)
+      timeout -k 10 400 python -u scripts/consensus_trace.py > ${O}_constrace.log 2>&1
+      rc=$?; tail -c 2500 ${O}_constrace.log; [ $rc -ne 0 ] && exit $rc ;;
     rs16ab)
       for i in 1 2 3; do
-        for lib in celestia-app_amd/cda/libcda.so ab/libcda_touch0.so; do
+        for lib in ${LIBS:-celestia-app_amd/cda/libcda.so ab/libcda_touch0.so ab/libcda_nt.so}; do
           echo "$lib $(CDA_LIB=$lib timeout -k 10 120 python scripts/rs16_probe.py 20)" >> ${O}_rs16ab.log || exit 1
         done
       done
@@ -34,3 +42,4 @@ for stage in "$@"; do
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done
+exit 0
