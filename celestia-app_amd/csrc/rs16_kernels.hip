@@ -665,52 +665,19 @@ __device__ __forceinline__ void prefetch01(const uint8_t* src, long long sh, int
     for (int q = 0; q < 4; q++) glds16(sp + 128 * q, base + (uint32_t)(r * 4 + q) * 1024u);
   }
 }
-// Round-ahead cache prefetch ("touch").  A persistent round = codewords [r G, (r + 1) G) of the launch (G = grid =
-// one workgroup per CU).  At the top of its codeword of round r, every workgroup pulls 1/G of round r + 1's input
-// -- 512 cells, 256 KiB -- from HBM into the caches (L2 / Infinity Cache) while it computes, so the loads of round r + 1
-// are cache hits instead of HBM misses taken in the memory phase that all CUs enter together.  The cells are dealt in
-// memory order: a column pass (codewords = adjacent cells, shards 2k cells apart) hands workgroup b two whole 128-KiB
-// row segments instead of 512 cells 512 KiB apart; a row pass hands it its own next row.  Each lane requests one dword
-// of each of two 128-B lines through the LDS-DMA path into a 256-B junk slot of its wave (no VGPR is written, so the
-// compiler's vmcnt bookkeeping is unaffected: these loads are issued before the round's prefetch DMA, whose counted
-// wait -- read_prefetch<N> -- therefore still needs no change).  CDA_RS16_TOUCH=0 builds the kernel without it (A/B).
-#ifndef CDA_RS16_TOUCH
-#define CDA_RS16_TOUCH 1
-#endif
-constexpr uint32_t kJunkBytes = 16 * 256;  // per-wave junk slots behind the 128 KiB exchange buffer
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void touch_round(const Args& a, int g_next, uint32_t junk_lds) {
-#if CDA_RS16_TOUCH
-  // one workgroup per CU of a 256-CU part and whole 512-B slices (the k = 512 square passes); anything else skips it
-  const int G = (int)gridDim.x, b = (int)blockIdx.x;
-  const int round0 = g_next - b;  // first codeword of the next round (uniform)
-  if (G != 256 || a.slices != 1 || a.cw_per_blk < G || round0 >= a.total) return;
-  const bool shard_major = a.src_sh <= a.src_cw;  // cells of a codeword contiguous (row pass): codeword-major chunks
-  const int cw0 = round0 % a.cw_per_blk, blk0 = round0 / a.cw_per_blk;  // uniform
-  const int tq = (int)threadIdx.x >> 2, tl = (int)threadIdx.x & 3;       // cell (of 256) and line (of 4) of a lane
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    // cell e = b * 512 + i * 256 + tq of the round's 256 x 512 cells in memory order
-    const int j = shard_major ? b : tq;               // codeword of the round
-    const int sh = shard_major ? i * 256 + tq : 2 * b + i;  // shard
-    int cw = cw0 + j, blk = blk0;
-    if (cw >= a.cw_per_blk) cw -= a.cw_per_blk, blk++;
-    if (round0 + j >= a.total) cw = 0, blk = 0;  // past the launch's last codeword: any valid cell
-    const uint8_t* p = a.src + blk * a.src_blk + cw * a.src_cw + sh * a.src_sh + tl * 128;
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" : : "v"(p), "s"(junk_lds) : "memory", "m0");
-  }
-#else
-  (void)a, (void)g_next, (void)junk_lds;
-#endif
-}
-#pragma clang diagnostic pop
 
-// Parity stores of the persistent loop.  CDA_RS16_NT_STORES=1 (A/B builds) marks them non-temporal: the bottom half
-// is read next by the leaf hashing, not by this kernel, so keeping it out of L2 could let the next round's cached
-// input stay there.
+// Parity stores of the persistent loop, non-temporal: nothing in this kernel reads them again (the leaf hashing does,
+// a launch later), and the store drain at each codeword's end is the part of the memory phase the next codeword waits
+// behind.  Same-box rotating A/B, 3 rounds (profiles/r05_rs16_ab.log, ms per square): columns 0.252-0.254 vs
+// 0.259-0.267, rows 0.129-0.131 vs 0.131-0.134.  CDA_RS16_NT_STORES=0 builds the plain stores (A/B).
+//
+// Measured and not kept (same log): a round-ahead cache prefetch -- each workgroup pulling 1/G of the next persistent
+// round's input (two 128-KiB row segments of the column pass, its own next row of the row pass) into L2 / the
+// Infinity Cache through LDS-DMA "touch" loads at the top of each codeword, so that the strided column reads would hit
+// the cache: columns 0.272-0.287 vs 0.259-0.267 ms per square without it, rows unchanged, memory-only builds
+// unchanged (0.117 / 0.052 ms).  The column pass's memory phase is not made shorter by moving its DRAM reads earlier.
 #ifndef CDA_RS16_NT_STORES
-#define CDA_RS16_NT_STORES 0
+#define CDA_RS16_NT_STORES 1
 #endif
 __device__ __forceinline__ void store_parity(uint4* o, const uint4& q0, const uint4& q1, const uint4& q2,
                                              const uint4& q3) {
@@ -836,10 +803,8 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
   }
   uint32_t E[4][16];
   top_part<OM, 8>(a, xw, w, g, cx, R, E);  // after the prologue only its 8 R loads follow the prefetch
-  const uint32_t junk = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr)(xb + 128 * 1024 / 16)) + w * 256;
   for (int it = 0;; it++) {
     rs16_mark(a, w, it, 0);
-    touch_round(a, g + (int)gridDim.x, junk);
 #pragma unroll
     for (int i = 0; i < 4; i++) asm volatile("" : "+v"(cx.lv[i]));
     asm volatile("" : "+v"(cx.lm3));
@@ -915,8 +880,7 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
 // one whole body per value of W1..W3 (scalar branch at entry; each runs to the end, so no control-flow merge with
 // the 64 live state registers follows the specialised layers -- such a merge made the register allocator spill)
 __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB,
-                                                              // then the touch loads' junk slots (kJunkBytes)
+  extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #if CDA_RS16_PIPE && CDA_RS16_DIAG_MODE == 0
 #define CDA_RS16_BODY body2
@@ -965,7 +929,7 @@ int rs16_reg_init(int device) {
     if (want != kCpoly16[i]) return -1;
   }
   return hipFuncSetAttribute((const void*)r16::rs_encode16_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             128 * 1024 + r16::kJunkBytes) == hipSuccess
+                             128 * 1024) == hipSuccess
              ? 0
              : -1;
 }
@@ -1004,8 +968,7 @@ int launch_rs_encode16_reg(const RsJob& j, const uint16_t* d_cpoly, hipStream_t 
     return n;
   }();
   const int grid = (int)(total < ncu ? total : ncu);
-  hipLaunchKernelGGL(r16::rs_encode16_reg_kernel, dim3((unsigned)grid), dim3(1024), 128 * 1024 + r16::kJunkBytes, s,
-                     a);
+  hipLaunchKernelGGL(r16::rs_encode16_reg_kernel, dim3((unsigned)grid), dim3(1024), 128 * 1024, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
