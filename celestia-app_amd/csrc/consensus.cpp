@@ -158,13 +158,19 @@ bool consensus_eligible(const cda_ctx* c, uint32_t k) { return c->consensus && !
 
 namespace {
 
-bool pinned_host(const void* p) {
+constexpr int kPushBlocks = 64;  // workgroups of each push kernel (256 threads)
+
+// Page-locked host memory (hipHostMalloc / hipHostRegister)?  *dev = the address the GPU writes it through.
+bool pinned_host(const void* p, void** dev) {
   hipPointerAttribute_t a{};
+  *dev = nullptr;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory is not an error here
     return false;
   }
-  return a.type == hipMemoryTypeHost;
+  if (a.type != hipMemoryTypeHost) return false;
+  *dev = a.devicePointer;
+  return true;
 }
 
 int grow_pinned(cda_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
@@ -327,7 +333,13 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)) || (rc = prepare_trees(c, k, 1, c->stream)))
     return rc;
   const bool want = eds_or_null != nullptr;
-  const bool out_pinned = want && pinned_host(eds_or_null);
+  void* eds_dev = nullptr;  // the page-locked caller buffer as the GPU addresses it
+  const bool out_pinned = want && pinned_host(eds_or_null, &eds_dev);
+  // page-locked output: Q1 and the bottom half are written into it by push kernels on the D2H stream (the CUs store
+  // across PCIe), so they overlap the input's DMA even where the DMA engines serialise the two directions; the input
+  // and the results keep the DMA engines.  cons_push = 0 (CDA_CONS_PUSH=0): DMA as for pageable buffers.
+  const bool push = out_pinned && eds_dev != nullptr && c->cons_push;
+  uint8_t* eds_d = (uint8_t*)eds_dev;
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
   const bool banded = in_mode_env ? in_mode_env == 1 : want;
@@ -341,7 +353,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const size_t stg_b = (want && !out_pinned) ? std::min(bot_b / 4 * 3, stg_want / (2 * erowS) * (2 * erowS)) : 0;
   const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
   const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
-  if ((want && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
+  if ((want && !push && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
       (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
     return rc;
   if (fresh && c->huge_pages) want_huge_pages(eds_or_null, eds_b);  // opt-in only (cda_set_option)
@@ -386,7 +398,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
           }
         });
       }
-    for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its DMA into the slab has landed
+    for (uint32_t b = 0; b < nband && !push; b++)  // Q1 rows of band b, once its DMA into the slab has landed
         for (uint32_t r0 = b * kb; r0 < (b + 1) * kb; r0 += rows_per_task)
           tasks.emplace_back([=, &q1_rec, &abort] {
             if (!wait_count(q1_rec, (int)b + 1, abort) || !wait_event(X->ev_q1[b], abort)) return;
@@ -447,11 +459,19 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       fail = "rows";
       break;
     }
-    if (want) {
-      // Q1 lands contiguously in the pinned slab whatever the caller's buffer is: a DMA into the strided right halves
-      // of the caller's rows ran at half the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, whether the
-      // caller's memory is pinned or not; a strided DEVICE source costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py,
-      // profiles/r05_pcie_duplex.log), so the pool moves the rows into place host to host.
+    if (want && push) {  // Q1 of the band straight into the caller's rows, by the push kernel
+      if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
+          hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
+          launch_push_rows(d_eds + r0 * erowS + rowS, erowS, eds_d + r0 * erowS + rowS, erowS, rowS, kb,
+                           kPushBlocks, c->d2h_stream) != 0) {
+        fail = "Q1 push";
+        break;
+      }
+    } else if (want) {
+      // Q1 lands contiguously in the pinned slab: a DMA into the strided right halves of the caller's rows ran at
+      // half the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, pinned caller memory too; a strided
+      // DEVICE source costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py, profiles/r05_pcie_duplex.log), so the
+      // pool moves the rows into place host to host.
       uint8_t* dst = X->pin_out + r0 * rowS;
       const size_t dpitch = rowS;
       if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
@@ -476,7 +496,10 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   if (!fail && want &&
       (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess))
     fail = "event";
-  if (!fail && out_pinned &&
+  if (!fail && push && launch_push_rows(d_eds + k * erowS, bot_b, eds_d + k * erowS, bot_b, bot_b, 1, kPushBlocks,
+                                        c->d2h_stream) != 0)
+    fail = "bottom push";
+  if (!fail && out_pinned && !push &&
       hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
           hipSuccess)
     fail = "bottom D2H";

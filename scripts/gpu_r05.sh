@@ -21,8 +21,14 @@ for stage in "$@"; do
       timeout -k 10 400 python -u scripts/consensus_shapes.py 25 3 > ${O}_shapes.log 2>&1
       rc=$?; tail -c 2500 ${O}_shapes.log; [ $rc -ne 0 ] && exit $rc ;;
     duplex)
-      timeout -k 10 120 python -u scripts/pcie_duplex_probe.py > ${O}_duplex.log 2>&1
-      rc=$?; tail -c 1000 ${O}_duplex.log; [ $rc -ne 0 ] && exit $rc ;;
+      for i in 1 2; do
+        timeout -k 10 120 python -u scripts/pcie_duplex_probe.py >> ${O}_duplex.log 2>&1 || exit 1
+        HSA_ENABLE_SDMA=0 timeout -k 10 120 python -u scripts/pcie_duplex_probe.py | sed 's/^{/{"sdma": 0, /' >> ${O}_duplex.log 2>&1 || exit 1
+      done
+      grep '^{' ${O}_duplex.log ;;
+    constrace_blit)
+      HSA_ENABLE_SDMA=0 timeout -k 10 400 python -u scripts/consensus_trace.py > ${O}_constrace_blit.log 2>&1
+      rc=$?; tail -c 2500 ${O}_constrace_blit.log; [ $rc -ne 0 ] && exit $rc ;;
     constrace)
       timeout -k 10 400 python -u scripts/consensus_trace.py > ${O}_constrace.log 2>&1
       rc=$?; tail -c 2500 ${O}_constrace.log; [ $rc -ne 0 ] && exit $rc ;;
