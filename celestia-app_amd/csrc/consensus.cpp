@@ -337,7 +337,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const bool out_pinned = want && pinned_host(eds_or_null, &eds_dev);
   // page-locked output: Q1 and the bottom half are written into it by push kernels on the D2H stream (the CUs store
   // across PCIe), so they overlap the input's DMA even where the DMA engines serialise the two directions; the input
-  // and the results keep the DMA engines.  cons_push = 0 (CDA_CONS_PUSH=0): DMA as for pageable buffers.
+  // and the results keep the DMA engines.  Off by default (cons_push, CDA_CONS_PUSH=1): measured slower.
   const bool push = out_pinned && eds_dev != nullptr && c->cons_push;
   uint8_t* eds_d = (uint8_t*)eds_dev;
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
@@ -441,6 +441,29 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   int frc = CDA_OK;
   // the order-status word is set on the compute stream while the input is still coming up (off the chain)
   if (hipMemsetAsync(d_status, 0xFF, 8, s) != hipSuccess) fail = "status";
+  // Q1 of band b back to the host once its row pass has run (D2H stream)
+  auto issue_q1 = [&](uint32_t b) -> bool {
+    const size_t r0 = (size_t)b * kb;
+    if (hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess) return false;
+    if (push)  // straight into the caller's rows, by the push kernel
+      return launch_push_rows(d_eds + r0 * erowS + rowS, erowS, eds_d + r0 * erowS + rowS, erowS, rowS, kb,
+                              kPushBlocks, c->d2h_stream) == 0;
+    // Q1 lands contiguously in the pinned slab: a DMA into the strided right halves of the caller's rows ran at half
+    // the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, pinned caller memory too; a strided DEVICE source
+    // costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py, profiles/r05_pcie_duplex.log), so the pool moves the rows
+    // into place host to host.
+    if (hipMemcpy2DAsync(X->pin_out + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
+                         hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
+        hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess)
+      return false;
+    q1_rec.store((int)b + 1, std::memory_order_release);
+    return true;
+  };
+  // cons_order = 1: every input band's DMA is submitted before any Q1 copy.  Where the DMA engines run the two
+  // directions one after the other in submission order, a Q1 copy queued between two input bands waits for its row
+  // pass and holds the next band back (profiles/r05_consensus_trace_v1.log: the column pass ends at ~0.3 ms instead
+  // of ~0.18); where they overlap, interleaving starts the D2H earlier.
+  const bool inputs_first = c->cons_order == 1;
   for (uint32_t b = 0; b < nband && !fail; b++) {  // device work, band by band as the input lands
     const size_t r0 = (size_t)b * kb;
     if (hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
@@ -459,32 +482,13 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       fail = "rows";
       break;
     }
-    if (want && push) {  // Q1 of the band straight into the caller's rows, by the push kernel
-      if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
-          hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
-          launch_push_rows(d_eds + r0 * erowS + rowS, erowS, eds_d + r0 * erowS + rowS, erowS, rowS, kb,
-                           kPushBlocks, c->d2h_stream) != 0) {
-        fail = "Q1 push";
-        break;
-      }
-    } else if (want) {
-      // Q1 lands contiguously in the pinned slab: a DMA into the strided right halves of the caller's rows ran at
-      // half the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, pinned caller memory too; a strided
-      // DEVICE source costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py, profiles/r05_pcie_duplex.log), so the
-      // pool moves the rows into place host to host.
-      uint8_t* dst = X->pin_out + r0 * rowS;
-      const size_t dpitch = rowS;
-      if (hipEventRecord(X->ev_rows[b], s) != hipSuccess ||
-          hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
-          hipMemcpy2DAsync(dst, dpitch, d_eds + r0 * erowS + rowS, erowS, rowS, kb, hipMemcpyDeviceToHost,
-                           c->d2h_stream) != hipSuccess ||
-          hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess) {
-        fail = "Q1 D2H";
-        break;
-      }
-      q1_rec.store((int)b + 1, std::memory_order_release);
+    if (want && (hipEventRecord(X->ev_rows[b], s) != hipSuccess || (!inputs_first && !issue_q1(b)))) {
+      fail = "Q1 D2H";
+      break;
     }
   }
+  for (uint32_t b = 0; b < nband && !fail && want && inputs_first; b++)
+    if (!issue_q1(b)) fail = "Q1 D2H";
   mark(2);
   if (!fail) {
     const RsJob j = cols_job(k, 1, d_eds);
