@@ -131,14 +131,16 @@ struct Consensus {
   uint8_t* pin_out = nullptr;  // Q1 (k x k shares) of a pageable output
   uint8_t* pin_res = nullptr;  // 4k root records | DAH | status
   uint8_t* d_res = nullptr;    // the same on the device: one D2H of the results
-  size_t cap_out = 0, cap_res = 0, cap_dres = 0;
+  uint8_t* d_q1 = nullptr;     // Q1 gathered contiguously on the device before its D2H (q1_gather)
+  size_t cap_out = 0, cap_res = 0, cap_dres = 0, cap_dq1 = 0;
   hipEvent_t ev_in[kMaxBands] = {}, ev_rows[kMaxBands] = {}, ev_q1[kMaxBands] = {}, ev_cols = nullptr,
              ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr, ev_stg[kMaxPieces] = {};
   ~Consensus() {
     delete pool;
     for (uint8_t* p : {pin_out, pin_res})
       if (p) (void)hipHostFree(p);
-    if (d_res) (void)hipFree(d_res);
+    for (uint8_t* p : {d_res, d_q1})
+      if (p) (void)hipFree(p);
     for (int i = 0; i < kMaxBands; i++)
       for (hipEvent_t e : {ev_in[i], ev_rows[i], ev_q1[i]})
         if (e) (void)hipEventDestroy(e);
@@ -354,7 +356,8 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
   const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
   if ((want && !push && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
-      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
+      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)) ||
+      (want && c->cons_q1_gather && (rc = grow_device(c, X->d_q1, X->cap_dq1, q1_b))))
     return rc;
   if (fresh && c->huge_pages) want_huge_pages(eds_or_null, eds_b);  // opt-in only (cda_set_option)
   uint8_t* d_ods = (uint8_t*)c->ods.p;
@@ -452,10 +455,20 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
     // the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, pinned caller memory too; a strided DEVICE source
     // costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py, profiles/r05_pcie_duplex.log), so the pool moves the rows
     // into place host to host.
-    if (hipMemcpy2DAsync(X->pin_out + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
-                         hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
-        hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess)
+    // (q1_gather: the band's strided right halves are first gathered into a contiguous device buffer, then one
+    // contiguous D2H -- the 2-D D2H ran at ~44 GB/s in the kernel + copy trace, a contiguous one at ~56,
+    // profiles/r05_consensus_trace_prof.txt)
+    if (c->cons_q1_gather) {
+      if (hipMemcpy2DAsync(X->d_q1 + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
+                           hipMemcpyDeviceToDevice, c->d2h_stream) != hipSuccess ||
+          hipMemcpyAsync(X->pin_out + r0 * rowS, X->d_q1 + r0 * rowS, (size_t)kb * rowS, hipMemcpyDeviceToHost,
+                         c->d2h_stream) != hipSuccess)
+        return false;
+    } else if (hipMemcpy2DAsync(X->pin_out + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
+                                hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess) {
       return false;
+    }
+    if (hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess) return false;
     q1_rec.store((int)b + 1, std::memory_order_release);
     return true;
   };
@@ -463,12 +476,19 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   // directions one after the other in submission order, a Q1 copy queued between two input bands waits for its row
   // pass and holds the next band back (profiles/r05_consensus_trace_v1.log: the column pass ends at ~0.3 ms instead
   // of ~0.18); where they overlap, interleaving starts the D2H earlier.
-  const bool inputs_first = c->cons_order == 1;
+  const bool inputs_first = c->cons_order >= 1;
+  // cons_order = 2: every input band's DMA is enqueued before the first row pass (back to back on the H2D stream)
+  auto issue_in = [&](uint32_t b) -> bool {
+    const size_t r0 = (size_t)b * kb;
+    return hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
+                          c->h2d_stream) == hipSuccess &&
+           hipEventRecord(X->ev_in[b], c->h2d_stream) == hipSuccess;
+  };
+  for (uint32_t b = 0; b < nband && !fail && c->cons_order == 2; b++)
+    if (!issue_in(b)) fail = "H2D";
   for (uint32_t b = 0; b < nband && !fail; b++) {  // device work, band by band as the input lands
     const size_t r0 = (size_t)b * kb;
-    if (hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
-                       c->h2d_stream) != hipSuccess ||
-        hipEventRecord(X->ev_in[b], c->h2d_stream) != hipSuccess || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
+    if ((c->cons_order != 2 && !issue_in(b)) || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
       fail = "H2D";
       break;
     }

@@ -29,11 +29,17 @@ for stage in "$@"; do
     consweep)  # one-block path forms (knobs read at cda_init), two rotations, plus the box's DMA duplex behaviour
       timeout -k 10 120 python -u scripts/pcie_duplex_probe.py > ${O}_consweep.log 2>&1 || exit 1
       for i in 1 2; do
-        for v in "CDA_CONS_ORDER=0" "CDA_CONS_ORDER=1" "CDA_CONS_ORDER=1 CDA_CONS_IN=2" "CDA_CONS_ORDER=0 CDA_CONS_IN=2" "CDA_CONS_PUSH=1 CDA_CONS_ORDER=1"; do
+        for v in ${CONS_FORMS:-"CDA_CONS_ORDER=0" "CDA_CONS_ORDER=1" "CDA_CONS_ORDER=1 CDA_CONS_IN=2" "CDA_CONS_ORDER=0 CDA_CONS_IN=2" "CDA_CONS_PUSH=1 CDA_CONS_ORDER=1"}; do
           echo "== $v $(env $v timeout -k 10 200 python -u scripts/consensus_trace.py | grep '^{')" >> ${O}_consweep.log || exit 1
         done
       done
       cat ${O}_consweep.log | cut -c 1-400 ;;
+    constrace_prof)  # rocprofv3 kernel + memory-copy trace of pinned one-block calls (no PMC in this run)
+      mkdir -p gpurun_out/prof_cons
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+        -d $GRAFT_REPO_ROOT/gpurun_out/prof_cons -o run -- python3 $GRAFT_REPO_ROOT/scripts/consensus_calls.py 40) \
+        > ${O}_constrace_prof.log 2>&1
+      rc=$?; tail -n 5 ${O}_constrace_prof.log; find gpurun_out/prof_cons -name "*.csv" | head; [ $rc -ne 0 ] && exit $rc ;;
     constrace_blit)
       HSA_ENABLE_SDMA=0 timeout -k 10 400 python -u scripts/consensus_trace.py > ${O}_constrace_blit.log 2>&1
       rc=$?; tail -c 2500 ${O}_constrace_blit.log; [ $rc -ne 0 ] && exit $rc ;;
