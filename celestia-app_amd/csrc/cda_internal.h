@@ -121,9 +121,6 @@ int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t
                        void* d_out, void* d_nodes_out, hipStream_t s);
 
 // ODS of a share plan (square_kernels.hip), one thread per 16-B word; -2: empty plan
-// CU-driven copy of pitched device rows into GPU-addressable page-locked host memory (square_kernels.hip)
-int launch_push_rows(const void* d_src, size_t src_pitch, void* h_dst_dev, size_t dst_pitch, size_t row_bytes,
-                     uint32_t rows, int nblocks, hipStream_t s);
 int launch_scatter_cell_runs(const void* d_compact, void* d_dst, const uint32_t* d_dst_cell, const uint32_t* d_pre,
                              int nruns, uint32_t ncells, hipStream_t s);
 int launch_build_ods(const cda_share_segment* d_segs, int nseg, const uint8_t* d_data, const uint32_t* d_reserved,

@@ -131,16 +131,14 @@ struct Consensus {
   uint8_t* pin_out = nullptr;  // Q1 (k x k shares) of a pageable output
   uint8_t* pin_res = nullptr;  // 4k root records | DAH | status
   uint8_t* d_res = nullptr;    // the same on the device: one D2H of the results
-  uint8_t* d_q1 = nullptr;     // Q1 gathered contiguously on the device before its D2H (q1_gather)
-  size_t cap_out = 0, cap_res = 0, cap_dres = 0, cap_dq1 = 0;
+  size_t cap_out = 0, cap_res = 0, cap_dres = 0;
   hipEvent_t ev_in[kMaxBands] = {}, ev_rows[kMaxBands] = {}, ev_q1[kMaxBands] = {}, ev_cols = nullptr,
              ev_done = nullptr, ev_h2d_end = nullptr, ev_d2h_end = nullptr, ev_stg[kMaxPieces] = {};
   ~Consensus() {
     delete pool;
     for (uint8_t* p : {pin_out, pin_res})
       if (p) (void)hipHostFree(p);
-    for (uint8_t* p : {d_res, d_q1})
-      if (p) (void)hipFree(p);
+    if (d_res) (void)hipFree(d_res);
     for (int i = 0; i < kMaxBands; i++)
       for (hipEvent_t e : {ev_in[i], ev_rows[i], ev_q1[i]})
         if (e) (void)hipEventDestroy(e);
@@ -160,19 +158,14 @@ bool consensus_eligible(const cda_ctx* c, uint32_t k) { return c->consensus && !
 
 namespace {
 
-constexpr int kPushBlocks = 64;  // workgroups of each push kernel (256 threads)
-
-// Page-locked host memory (hipHostMalloc / hipHostRegister)?  *dev = the address the GPU writes it through.
-bool pinned_host(const void* p, void** dev) {
+// Page-locked host memory (hipHostMalloc / hipHostRegister)?
+bool pinned_host(const void* p) {
   hipPointerAttribute_t a{};
-  *dev = nullptr;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory is not an error here
     return false;
   }
-  if (a.type != hipMemoryTypeHost) return false;
-  *dev = a.devicePointer;
-  return true;
+  return a.type == hipMemoryTypeHost;
 }
 
 int grow_pinned(cda_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
@@ -335,13 +328,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)) || (rc = prepare_trees(c, k, 1, c->stream)))
     return rc;
   const bool want = eds_or_null != nullptr;
-  void* eds_dev = nullptr;  // the page-locked caller buffer as the GPU addresses it
-  const bool out_pinned = want && pinned_host(eds_or_null, &eds_dev);
-  // page-locked output: Q1 and the bottom half are written into it by push kernels on the D2H stream (the CUs store
-  // across PCIe), so they overlap the input's DMA even where the DMA engines serialise the two directions; the input
-  // and the results keep the DMA engines.  Off by default (cons_push, CDA_CONS_PUSH=1): measured slower.
-  const bool push = out_pinned && eds_dev != nullptr && c->cons_push;
-  uint8_t* eds_d = (uint8_t*)eds_dev;
+  const bool out_pinned = want && pinned_host(eds_or_null);
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
   const bool banded = in_mode_env ? in_mode_env == 1 : want;
@@ -355,9 +342,8 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const size_t stg_b = (want && !out_pinned) ? std::min(bot_b / 4 * 3, stg_want / (2 * erowS) * (2 * erowS)) : 0;
   const size_t dir_b = bot_b - stg_b;  // the pageable part, at the front of the bottom half
   const int n_stg = stg_b ? std::min(Consensus::kMaxPieces, std::max(1, (int)(stg_b >> 20))) : 0;
-  if ((want && !push && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
-      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)) ||
-      (want && c->cons_q1_gather && (rc = grow_device(c, X->d_q1, X->cap_dq1, q1_b))))
+  if ((want && (rc = grow_pinned(c, X->pin_out, X->cap_out, q1_b + stg_b))) ||
+      (rc = grow_pinned(c, X->pin_res, X->cap_res, res_b)) || (rc = grow_device(c, X->d_res, X->cap_dres, res_b)))
     return rc;
   if (fresh && c->huge_pages) want_huge_pages(eds_or_null, eds_b);  // opt-in only (cda_set_option)
   uint8_t* d_ods = (uint8_t*)c->ods.p;
@@ -401,7 +387,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
           }
         });
       }
-    for (uint32_t b = 0; b < nband && !push; b++)  // Q1 rows of band b, once its DMA into the slab has landed
+    for (uint32_t b = 0; b < nband; b++)  // Q1 rows of band b, once its DMA into the slab has landed
         for (uint32_t r0 = b * kb; r0 < (b + 1) * kb; r0 += rows_per_task)
           tasks.emplace_back([=, &q1_rec, &abort] {
             if (!wait_count(q1_rec, (int)b + 1, abort) || !wait_event(X->ev_q1[b], abort)) return;
@@ -444,51 +430,25 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   int frc = CDA_OK;
   // the order-status word is set on the compute stream while the input is still coming up (off the chain)
   if (hipMemsetAsync(d_status, 0xFF, 8, s) != hipSuccess) fail = "status";
-  // Q1 of band b back to the host once its row pass has run (D2H stream)
+  // Q1 of band b back to the host once its row pass has run (D2H stream).  It lands contiguously in the pinned slab
+  // and the pool moves the rows into the caller's buffer: a DMA into the strided right halves of the caller's rows ran
+  // at about half the link rate (8 MiB: 0.31-0.40 ms against 0.16 ms contiguous, pinned caller memory too; a strided
+  // DEVICE source costs nothing: 0.17 ms; scripts/pcie_duplex_probe.py, profiles/r05_pcie_duplex.log).
   auto issue_q1 = [&](uint32_t b) -> bool {
     const size_t r0 = (size_t)b * kb;
-    if (hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess) return false;
-    if (push)  // straight into the caller's rows, by the push kernel
-      return launch_push_rows(d_eds + r0 * erowS + rowS, erowS, eds_d + r0 * erowS + rowS, erowS, rowS, kb,
-                              kPushBlocks, c->d2h_stream) == 0;
-    // Q1 lands contiguously in the pinned slab: a DMA into the strided right halves of the caller's rows ran at half
-    // the link rate (8 MiB: 0.31-0.36 ms against 0.16 ms contiguous, pinned caller memory too; a strided DEVICE source
-    // costs nothing: 0.17 ms, scripts/pcie_duplex_probe.py, profiles/r05_pcie_duplex.log), so the pool moves the rows
-    // into place host to host.
-    // (q1_gather: the band's strided right halves are first gathered into a contiguous device buffer, then one
-    // contiguous D2H -- the 2-D D2H ran at ~44 GB/s in the kernel + copy trace, a contiguous one at ~56,
-    // profiles/r05_consensus_trace_prof.txt)
-    if (c->cons_q1_gather) {
-      if (hipMemcpy2DAsync(X->d_q1 + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
-                           hipMemcpyDeviceToDevice, c->d2h_stream) != hipSuccess ||
-          hipMemcpyAsync(X->pin_out + r0 * rowS, X->d_q1 + r0 * rowS, (size_t)kb * rowS, hipMemcpyDeviceToHost,
-                         c->d2h_stream) != hipSuccess)
-        return false;
-    } else if (hipMemcpy2DAsync(X->pin_out + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
-                                hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess) {
+    if (hipStreamWaitEvent(c->d2h_stream, X->ev_rows[b], 0) != hipSuccess ||
+        hipMemcpy2DAsync(X->pin_out + r0 * rowS, rowS, d_eds + r0 * erowS + rowS, erowS, rowS, kb,
+                         hipMemcpyDeviceToHost, c->d2h_stream) != hipSuccess ||
+        hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess)
       return false;
-    }
-    if (hipEventRecord(X->ev_q1[b], c->d2h_stream) != hipSuccess) return false;
     q1_rec.store((int)b + 1, std::memory_order_release);
     return true;
   };
-  // cons_order = 1: every input band's DMA is submitted before any Q1 copy.  Where the DMA engines run the two
-  // directions one after the other in submission order, a Q1 copy queued between two input bands waits for its row
-  // pass and holds the next band back (profiles/r05_consensus_trace_v1.log: the column pass ends at ~0.3 ms instead
-  // of ~0.18); where they overlap, interleaving starts the D2H earlier.
-  const bool inputs_first = c->cons_order >= 1;
-  // cons_order = 2: every input band's DMA is enqueued before the first row pass (back to back on the H2D stream)
-  auto issue_in = [&](uint32_t b) -> bool {
-    const size_t r0 = (size_t)b * kb;
-    return hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
-                          c->h2d_stream) == hipSuccess &&
-           hipEventRecord(X->ev_in[b], c->h2d_stream) == hipSuccess;
-  };
-  for (uint32_t b = 0; b < nband && !fail && c->cons_order == 2; b++)
-    if (!issue_in(b)) fail = "H2D";
   for (uint32_t b = 0; b < nband && !fail; b++) {  // device work, band by band as the input lands
     const size_t r0 = (size_t)b * kb;
-    if ((c->cons_order != 2 && !issue_in(b)) || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
+    if (hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
+                       c->h2d_stream) != hipSuccess ||
+        hipEventRecord(X->ev_in[b], c->h2d_stream) != hipSuccess || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
       fail = "H2D";
       break;
     }
@@ -502,13 +462,11 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       fail = "rows";
       break;
     }
-    if (want && (hipEventRecord(X->ev_rows[b], s) != hipSuccess || (!inputs_first && !issue_q1(b)))) {
+    if (want && (hipEventRecord(X->ev_rows[b], s) != hipSuccess || !issue_q1(b))) {
       fail = "Q1 D2H";
       break;
     }
   }
-  for (uint32_t b = 0; b < nband && !fail && want && inputs_first; b++)
-    if (!issue_q1(b)) fail = "Q1 D2H";
   mark(2);
   if (!fail) {
     const RsJob j = cols_job(k, 1, d_eds);
@@ -520,10 +478,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   if (!fail && want &&
       (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess))
     fail = "event";
-  if (!fail && push && launch_push_rows(d_eds + k * erowS, bot_b, eds_d + k * erowS, bot_b, bot_b, 1, kPushBlocks,
-                                        c->d2h_stream) != 0)
-    fail = "bottom push";
-  if (!fail && out_pinned && !push &&
+  if (!fail && out_pinned &&
       hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
           hipSuccess)
     fail = "bottom D2H";

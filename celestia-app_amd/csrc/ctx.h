@@ -77,14 +77,6 @@ struct cda_ctx {
   // (CDA_CONS_OUT); cons_stg_mib: MiB of the bottom half staged through the pinned slab, -1 = default (CDA_CONS_STG);
   // cons_trace: phase timestamps to stderr (CDA_CONS_TRACE); copy_threads: pool size (CDA_COPY_THREADS).
   int cons_in = 0, cons_out = 0, cons_stg_mib = -1, copy_threads = 7;
-  // page-locked output: Q1 and the bottom half written by push kernels (CU stores across PCIe) instead of DMA
-  // (CDA_CONS_PUSH=1; measured slower, r05)
-  bool cons_push = false;
-  // 1: submit every input band's DMA before the Q1 copies, 2: and before the first row pass (CDA_CONS_ORDER);
-  // 0: interleaved band by band
-  int cons_order = 0;
-  // Q1 gathered into a contiguous device buffer before one contiguous D2H per band (CDA_CONS_Q1_GATHER)
-  bool cons_q1_gather = true;
   bool cons_trace = false;
   // Transparent huge pages for a fresh (never-touched) caller output buffer: madvise(MADV_HUGEPAGE) on its 2 MiB-aligned
   // interior before the copy pool touches it.  OFF by default: the hint changes the page policy of memory

@@ -339,9 +339,6 @@ int cda_init(int device, cda_ctx** out) {
   if (const char* e = getenv("CDA_CONS_STG")) c->cons_stg_mib = std::max(0, atoi(e));
   if (const char* e = getenv("CDA_COPY_THREADS")) c->copy_threads = std::max(1, std::min(64, atoi(e)));
   if (const char* e = getenv("CDA_HUGE_PAGES")) c->huge_pages = atoi(e) != 0;
-  if (const char* e = getenv("CDA_CONS_PUSH")) c->cons_push = atoi(e) != 0;
-  if (const char* e = getenv("CDA_CONS_ORDER")) c->cons_order = std::max(0, std::min(2, atoi(e)));
-  if (const char* e = getenv("CDA_CONS_Q1_GATHER")) c->cons_q1_gather = atoi(e) != 0;
   c->cons_trace = getenv("CDA_CONS_TRACE") != nullptr;
   find_local_cpus(c);
   // the streams that overlap each other, created right after `stream` so that they land on distinct hardware

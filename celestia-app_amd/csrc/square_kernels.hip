@@ -105,32 +105,6 @@ __global__ void __launch_bounds__(256) scatter_cell_runs_kernel(const uint4* __r
   dst[((size_t)dst_cell[lo] + (cell - pre[lo])) * 32 + (t & 31)] = compact[t];
 }
 
-// Device -> page-locked host copy done by the CUs (the one-block consensus path, csrc/consensus.cpp): `rows` rows of
-// `row_bytes` (a multiple of 16) from a pitched device region into a pitched region of host memory the GPU can address
-// (hipHostMalloc / hipHostRegister, through its device pointer).  The stores cross PCIe as posted writes.  On boxes
-// whose DMA engines run a host-to-device and a device-to-host copy one after the other (profiles/r05_pcie_duplex.log:
-// 8 MiB up + 24 MiB down 0.81 ms together against 0.16 + 0.45 ms alone), the device-to-host half of the call moves
-// here so that it overlaps the input's DMA.  A few workgroups, grid-stride over 16-B words: the call's compute kernels
-// keep the rest of the chip.
-__global__ void __launch_bounds__(256) push_rows_kernel(const uint4* __restrict__ src, size_t src_pitch16,
-                                                        uint4* __restrict__ dst, size_t dst_pitch16, uint32_t row_words,
-                                                        uint64_t nwords) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t r = i / row_words, c = i - r * row_words;
-    dst[r * dst_pitch16 + c] = src[r * src_pitch16 + c];
-  }
-}
-
-int launch_push_rows(const void* d_src, size_t src_pitch, void* h_dst_dev, size_t dst_pitch, size_t row_bytes,
-                     uint32_t rows, int nblocks, hipStream_t s) {
-  if (rows == 0 || row_bytes == 0) return 0;
-  if (row_bytes % 16 || src_pitch % 16 || dst_pitch % 16 || ((uintptr_t)d_src | (uintptr_t)h_dst_dev) % 16) return -2;
-  const uint64_t nwords = (uint64_t)rows * (row_bytes / 16);
-  hipLaunchKernelGGL(push_rows_kernel, dim3((unsigned)nblocks), dim3(256), 0, s, (const uint4*)d_src, src_pitch / 16,
-                     (uint4*)h_dst_dev, dst_pitch / 16, (uint32_t)(row_bytes / 16), nwords);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 int launch_scatter_cell_runs(const void* d_compact, void* d_dst, const uint32_t* d_dst_cell, const uint32_t* d_pre,
                              int nruns, uint32_t ncells, hipStream_t s) {
   if (nruns <= 0 || ncells == 0) return 0;

@@ -30,7 +30,7 @@ for stage in "$@"; do
       timeout -k 10 120 python -u scripts/pcie_duplex_probe.py > ${O}_consweep.log 2>&1 || exit 1
       for i in 1 2; do
         for v in ${CONS_FORMS:-"CDA_CONS_ORDER=0" "CDA_CONS_ORDER=1" "CDA_CONS_ORDER=1 CDA_CONS_IN=2" "CDA_CONS_ORDER=0 CDA_CONS_IN=2" "CDA_CONS_PUSH=1 CDA_CONS_ORDER=1"}; do
-          echo "== $v $(env $v timeout -k 10 200 python -u scripts/consensus_trace.py | grep '^{')" >> ${O}_consweep.log || exit 1
+          echo "== $v $(env ${v//,/ } timeout -k 10 200 python -u scripts/consensus_trace.py | grep '^{')" >> ${O}_consweep.log || exit 1
         done
       done
       cat ${O}_consweep.log | cut -c 1-400 ;;
