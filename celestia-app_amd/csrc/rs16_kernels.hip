@@ -646,6 +646,9 @@ __device__ __forceinline__ void from_state(const uint32_t (&Er)[16], uint32_t m1
 // behind a counted wait: exactly kAfterPrefetch vector-memory instructions of this wave follow the 8 DMA loads in
 // program order (the 16 parity stores and the 8 loads of r = 2, 3 of the store phase), so vmcnt(24) is the wait
 // for the prefetch alone.  The compiler's own waits for the r = 2, 3 loads then stay partial.
+// The counts are checked on the built code object, over every control-flow path from each prefetch to its wait
+// (tools/vmcnt_check.py, tests/test_rs16_vmcnt.py): a store or spill the compiler moved across would fail the build
+// check instead of racing.
 constexpr int kAfterPrefetch = 24;  // in the loop; 8 (the R loads) after the prologue's prefetch
 // M0 is reserved by the compiler; nothing else in this kernel uses it (the only M0 writes in its ISA are these), and
 // the clobber still tells the compiler it changes.
