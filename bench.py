@@ -639,6 +639,10 @@ def one_block_fresh(ctx, ods, reps=25, warmup=3):
                             EDS written into one of two recycled page-locked slabs (go/cda's EDS pool: Go-heap slabs
                             registered once with cda_host_register and recycled through the garbage collector).
       pooled_both           pooled shares slab (flatten inside the timed region) + pooled EDS slab.
+      pooled_eds_inplace    go/cda's ExtendShares: the shares flattened into Q0 of a pooled EDS slab (untimed, as the
+                            fresh share copy of the other series), then cda_extend_commit_eds in place: no share
+                            buffer, no host Q0 copy, the input bands are 2-D DMAs from page-locked memory.
+      pooled_eds_inplace_flatten  the same with the flatten inside the timed region (the Go call end to end).
       with_eds              fresh shares and a NEW never-touched EDS buffer per call (np.empty, as a Go make()), no
                             huge-page hint (the release default: the library does not change caller page policy).
       with_eds_hugepages    the same on a context that opted in (cda_set_option(CDA_OPT_HUGE_PAGES, 1)).
@@ -719,6 +723,26 @@ def one_block_fresh(ctx, ods, reps=25, warmup=3):
                 return ctx.extend_commit_batch(slab, eds_out=out)[3][0]
             return run
         series("pooled_both", pooled_both, lambda: last["out"][0])
+
+        def q0(buf):
+            return buf[0].reshape(2 * k, 2 * k, 512)[:k, :k]
+
+        def pooled_inplace(i):
+            out = pool_out[i % 2]
+            q0(out)[:] = ods.reshape(k, k, 512)  # the caller's flatten, straight into Q0 of the pooled slab
+            last["out"] = out
+            return lambda: ctx.extend_commit_eds(out[0])[2]
+        series("pooled_eds_inplace", pooled_inplace, lambda: last["out"][0])
+
+        def pooled_inplace_flatten(i):
+            out = pool_out[i % 2]
+            last["out"] = out
+
+            def run():
+                q0(out)[:] = ods.reshape(k, k, 512)
+                return ctx.extend_commit_eds(out[0])[2]
+            return run
+        series("pooled_eds_inplace_flatten", pooled_inplace_flatten, lambda: last["out"][0])
     finally:
         for b in pool_in + pool_out:
             ctx.host_unregister(b)
@@ -1275,7 +1299,7 @@ def gpu_vs_cpu(result, value):
         if hb.get("with_eds"):
             out["single_block_host_buffers_with_eds"] = round(best_cpu / hb["with_eds"], 1)
         fr = result.get("host_buffers", {}).get("one_block_fresh", {})
-        for key in ("roots_only", "pooled_eds", "pooled_both", "with_eds"):
+        for key in ("roots_only", "pooled_eds", "pooled_eds_inplace", "pooled_both", "with_eds"):
             if fr.get(key):
                 out[f"single_block_{key}_median"] = round(best_cpu / fr[key]["ms_median"], 1)
     c4 = cb.get("repair_c4_ms", {})

@@ -47,7 +47,7 @@ AXIS_COL = 1
 EXPORTS = [
     "cda_init", "cda_free", "cda_strerror", "cda_last_device_error", "cda_build_info",
     "cda_rs_encode", "cda_rs_decode", "cda_rs_max_chunks", "cda_rs_name", "cda_rs_validate_chunk_size",
-    "cda_extend_commit", "cda_extend_commit_batch", "cda_extend_commit_device", "cda_commit_eds",
+    "cda_extend_commit", "cda_extend_commit_batch", "cda_extend_commit_device", "cda_commit_eds", "cda_extend_commit_eds",
     "cda_dah_hash", "cda_nmt_axis_root", "cda_repair", "cda_repair_device",
     "cda_rs_encode_device", "cda_nmt_roots_device", "cda_nmt_fold_device", "cda_dah_device",
     "cda_profile_enable", "cda_profile_read", "cda_profile_reset",
@@ -115,6 +115,7 @@ def lib(path=None):
                 "cda_extend_commit_batch": (I32, [P, U32, U32, P, P, P, P, P, P]),
                 "cda_extend_commit_device": (I32, [P, U32, U32, P, P, P, P, P, P]),
                 "cda_commit_eds": (I32, [P, U32, P, P, P, P, P]),
+                "cda_extend_commit_eds": (I32, [P, U32, P, P, P, P, P]),
                 "cda_dah_hash": (I32, [P, U32, P, P, P]),
                 "cda_nmt_axis_root": (I32, [P, U64, U64, U32, U32, P, P, P]),
                 "cda_repair": (I32, [P, U32, P, P, P, P, P]),
@@ -305,6 +306,23 @@ class Context:
         rc = self._L.cda_dah_device(self._h, n_total, ctypes.c_void_p(d_roots), ctypes.c_void_p(d_dah),
                                   ctypes.c_void_p(stream or 0))
         _check(rc, ctx=self)
+
+    def extend_commit_eds(self, eds):
+        """In place (cda_extend_commit_eds): eds (4k^2, 512) uint8, C-contiguous, with the ODS in its top-left quadrant
+        (row r of the ODS = eds[r * 2k : r * 2k + k]); Q1..Q3 are written around it.  -> (row_roots, col_roots, dah)."""
+        if not (isinstance(eds, np.ndarray) and eds.dtype == np.uint8 and eds.flags.c_contiguous and eds.ndim == 2
+                and eds.shape[1] == SHARE_SIZE):
+            raise ValueError("eds must be a C-contiguous (4k^2, 512) uint8 array")
+        w = int(round(eds.shape[0] ** 0.5))
+        if w * w != eds.shape[0] or w % 2:
+            raise ValueError(f"eds holds {eds.shape[0]} shares, not a (2k)^2 square")
+        rr = np.empty((w, NODE_SIZE), np.uint8)
+        cr = np.empty((w, NODE_SIZE), np.uint8)
+        dah = np.empty(32, np.uint8)
+        err = ErrInfo()
+        _check(self._L.cda_extend_commit_eds(self._h, w // 2, _p(eds), _p(rr), _p(cr), _p(dah), ctypes.byref(err)),
+               err, self)
+        return rr, cr, dah.tobytes()
 
     def commit_eds(self, eds):
         eds = np.ascontiguousarray(eds, np.uint8)

@@ -307,8 +307,12 @@ void want_huge_pages(uint8_t* p, size_t n) {
 // Q0 is always the host copy of the caller's shares.  A/B forms (ctx fields read once at cda_init, ctx.h):
 // cons_in = 1 (bands) / 2 (one copy), cons_out = 2 (the resident form on any pageable buffer), cons_trace (phase
 // timestamps), cons_stg_mib.  A fresh output gets the huge-page hint only when the caller opted in (huge_pages).
+//
+// In place (cda_extend_commit_eds): the ODS is Q0 of the caller's EDS buffer (pitch 2k x 512), so there is no Q0 copy
+// and each input band is one 2-D DMA from the caller's rows (as fast as a contiguous one from page-locked memory:
+// 0.154 vs 0.155 ms per 8 MiB, scripts/h2d_2d_probe.py, profiles/r05_h2d_2d.log).
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
-                    uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+                    uint8_t* col_roots, uint8_t* dah, cda_err_info* err, size_t ods_pitch) {
   const int in_mode_env = c->cons_in, out_mode = c->cons_out;
   const bool trace = c->cons_trace;
   double tr[8] = {0};
@@ -321,6 +325,9 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const size_t ods_b = (size_t)k * rowS, eds_b = (size_t)w * erowS, q1_b = ods_b, bot_b = (size_t)k * erowS;
   const size_t roots_b = (size_t)2 * w * CDA_REC_BYTES, res_b = roots_b + 32 + 8;
   const size_t cells = (size_t)w * w;
+  if (!ods_pitch) ods_pitch = rowS;
+  const bool inplace = ods == eds_or_null;
+  if ((inplace && ods_pitch != erowS) || (!inplace && ods_pitch != rowS)) return CDA_E_ARG;
   Consensus* X = nullptr;
   int rc;
   if ((rc = ensure_pipeline(c)) || (rc = get_consensus(c, X)) || (rc = ensure(c, c->ods, ods_b)) ||
@@ -332,6 +339,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
   const bool banded = in_mode_env ? in_mode_env == 1 : want;
+
   // A pageable output's bottom half comes down in two concurrent parts: the front by pageable DMA on the D2H stream,
   // the back through the pinned slab on the second stream, copied out by the pool chunk by chunk as it lands.  The
   // pageable DMA alone ran at 36-46 GB/s; side by side the two fill the link.  Staged share, same box
@@ -374,16 +382,16 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       });
     }
     // Q0 = the shares, host to host (and the first touch of each row's Q1 half); a task covers 1 MiB of EDS rows at
-    // k = 128, the even tasks first so that the first faults land on distinct huge pages
+    // k = 128, the even tasks first so that the first faults land on distinct huge pages.  In place: Q0 is there.
     const uint32_t rows_per_task = std::max<uint32_t>(1, (uint32_t)(((size_t)512 << 10) / rowS));
     const uint32_t n_q0 = (k + rows_per_task - 1) / rows_per_task;
-    for (uint32_t half = 0; half < 2; half++)
+    for (uint32_t half = 0; half < 2 && (fresh || !inplace); half++)
       for (uint32_t t = half; t < n_q0; t += 2) {
         const uint32_t r0 = t * rows_per_task;
         tasks.emplace_back([=] {
           for (uint32_t r = r0; r < std::min(k, r0 + rows_per_task); r++) {
             if (fresh) touch_pages(eds_or_null + r * erowS + rowS, rowS);
-            memcpy(eds_or_null + r * erowS, ods + r * rowS, rowS);
+            if (!inplace) memcpy(eds_or_null + r * erowS, ods + r * rowS, rowS);
           }
         });
       }
@@ -446,9 +454,15 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   };
   for (uint32_t b = 0; b < nband && !fail; b++) {  // device work, band by band as the input lands
     const size_t r0 = (size_t)b * kb;
-    if (hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS, hipMemcpyHostToDevice,
-                       c->h2d_stream) != hipSuccess ||
-        hipEventRecord(X->ev_in[b], c->h2d_stream) != hipSuccess || hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
+    // (a page-locked input read by the row pass itself across PCIe, no DMA: 66 us per 2 MiB band against 44 us by
+    // DMA, 0.84 vs 0.74 ms per call; measured and removed, profiles/r05_consensus_timeline.log)
+    const hipError_t in_rc =
+        ods_pitch == rowS ? hipMemcpyAsync(d_ods + r0 * rowS, ods + r0 * rowS, (size_t)kb * rowS,
+                                           hipMemcpyHostToDevice, c->h2d_stream)
+                          : hipMemcpy2DAsync(d_ods + r0 * rowS, rowS, ods + r0 * ods_pitch, ods_pitch, rowS, kb,
+                                             hipMemcpyHostToDevice, c->h2d_stream);
+    if (in_rc != hipSuccess || hipEventRecord(X->ev_in[b], c->h2d_stream) != hipSuccess ||
+        hipStreamWaitEvent(s, X->ev_in[b], 0) != hipSuccess) {
       fail = "H2D";
       break;
     }
@@ -478,6 +492,9 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
   if (!fail && want &&
       (hipEventRecord(X->ev_cols, s) != hipSuccess || hipStreamWaitEvent(c->d2h_stream, X->ev_cols, 0) != hipSuccess))
     fail = "event";
+  // pinned output: the bottom half straight to it, one DMA behind the Q1 bands.  Device-to-host copies run one at a
+  // time whatever stream they are on (a second stream's copy started ~9 us after the first ended), so moving it to
+  // the idle input stream, whole or half, changed nothing (profiles/r05_consensus_timeline.log)
   if (!fail && out_pinned &&
       hipMemcpyAsync(eds_or_null + k * erowS, d_eds + k * erowS, bot_b, hipMemcpyDeviceToHost, c->d2h_stream) !=
           hipSuccess)

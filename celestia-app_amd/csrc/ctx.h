@@ -137,8 +137,10 @@ void bind_helper_thread(const cda_ctx* c);  // the calling helper thread -> c->l
 void find_local_cpus(cda_ctx* c);
 // one block through host buffers, overlapped with pinned staging and a copy pool (consensus.cpp; lock held)
 bool consensus_eligible(const cda_ctx* c, uint32_t k);
+// ods_pitch: bytes between ODS rows (0 = k * 512, contiguous); ods == eds_or_null with pitch 2k * 512 is the in-place
+// form (cda_extend_commit_eds: the caller's EDS buffer holds the ODS in Q0)
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
-                    uint8_t* col_roots, uint8_t* dah, cda_err_info* err);
+                    uint8_t* col_roots, uint8_t* dah, cda_err_info* err, size_t ods_pitch = 0);
 void free_consensus(cda_ctx* c);
 // RS jobs of the block path: rows (ODS row r -> Q0 copy + Q1 row r) and columns (top half -> bottom half)
 RsJob rows_job(uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds);

@@ -681,6 +681,28 @@ int cda_extend_commit(cda_ctx* c, uint32_t count, uint32_t share_len, const uint
   CDA_API_CATCH(c)
 }
 
+// In place: the ODS is Q0 of the caller's EDS buffer.  One block of k <= 256 takes the consensus path without its Q0
+// copy (the input bands are 2-D DMAs from the caller's rows); anything else (k = 512, profiling, a context without the
+// consensus path) gathers Q0 into a contiguous host copy and runs cda_extend_commit_batch, which writes Q0 back
+// unchanged.
+int cda_extend_commit_eds(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                          cda_err_info* err) {
+  CDA_API_TRY
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !eds || !row_roots || !col_roots || !dah) return CDA_E_ARG;
+  if (!is_pow2(k)) return set_err(err, CDA_E_NOT_POW2, -1, -1, -1, -1), CDA_E_NOT_POW2;
+  if (k > kMaxDeviceK) return CDA_E_UNSUPPORTED;
+  const size_t rowS = (size_t)k * CDA_SHARE, erowS = 2 * rowS;
+  {
+    Lock l(c);
+    if (consensus_eligible(c, k)) return extend_one_host(c, k, eds, eds, row_roots, col_roots, dah, err, erowS);
+  }
+  std::vector<uint8_t> ods((size_t)k * rowS);
+  for (uint32_t r = 0; r < k; r++) memcpy(ods.data() + r * rowS, eds + r * erowS, rowS);
+  return cda_extend_commit_batch(c, k, 1, ods.data(), eds, row_roots, col_roots, dah, err);
+  CDA_API_CATCH(c)
+}
+
 int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                    cda_err_info* err) {
   CDA_API_TRY

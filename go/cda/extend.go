@@ -34,21 +34,38 @@ func ExtendShares(s [][]byte) (*rsmt2d.ExtendedDataSquare, error) {
 	return ExtendSharesOn(mustDefault(), s)
 }
 
-// ExtendSharesOn is ExtendShares on a given context.  The shares are flattened into a pooled page-locked slab and
-// the EDS lands in a pooled page-locked slab that the returned square's cells live in (pool.go): both copies are
-// direct DMAs, the path csrc/consensus.cpp takes for pinned caller memory.
+// ExtendSharesOn is ExtendShares on a given context.  A square of 512-byte shares is flattened straight into Q0 of a
+// pooled page-locked EDS slab (pool.go) and extended in place by cda_extend_commit_eds: no separate share buffer, no
+// host copy of Q0, the input and output copies are direct DMAs, and the returned square's cells live in the slab.
+// Anything else (another share size, a count that is not a square) takes cda_extend_commit, which reports the
+// reference's errors in the reference's order.
 func ExtendSharesOn(ctx *Context, s [][]byte) (*rsmt2d.ExtendedDataSquare, error) {
 	if !isPowerOfTwo(len(s)) {
 		return nil, fmt.Errorf("number of shares is not a power of 2: got %d", len(s))
 	}
 	n := len(s[0])
+	k := squareSize(len(s))
+	w := 2 * k
+	if n == ShareSize && k*k == len(s) {
+		eds := takeEDS(ctx, w*w*n)
+		if err := flattenQ0(eds, s, k); err != nil {
+			return nil, err
+		}
+		rows := make([]byte, w*NodeSize)
+		cols := make([]byte, w*NodeSize)
+		dah := make([]byte, 32)
+		var info C.cda_err_info
+		rc := C.cda_extend_commit_eds(ctx.c, C.uint32_t(k), ptr(eds), ptr(rows), ptr(cols), ptr(dah), &info)
+		if rc != 0 {
+			return nil, toErr(rc, &info)
+		}
+		return importWithRoots(ctx, eds, w, n, rows, cols)
+	}
 	flat, arr := takeShares(ctx, len(s)*n)
 	defer giveShares(ctx, len(s)*n, arr)
 	if err := flattenInto(flat, s, n); err != nil {
 		return nil, err
 	}
-	k := squareSize(len(s))
-	w := 2 * k
 	eds := takeEDS(ctx, w*w*n)
 	rows := make([]byte, w*NodeSize)
 	cols := make([]byte, w*NodeSize)

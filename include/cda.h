@@ -117,6 +117,14 @@ int cda_extend_commit_batch(cda_ctx* ctx, uint32_t k, uint32_t nblocks, const ui
                             uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
                             cda_err_info* err);
 
+/* In-place form of cda_extend_commit for one k x k square: `eds` (4k^2*512 bytes, row-major) holds the ODS in its
+ * top-left quadrant Q0 (row r of the ODS at eds + r*2k*512); the call writes Q1..Q3 around it and returns the roots
+ * and DAH as cda_extend_commit.  rsmt2d's ComputeExtendedDataSquare builds the same square from the shares
+ * (pkg/da/data_availability_header.go:74); go/cda's ExtendShares flattens the shares straight into Q0 of a pooled
+ * page-locked EDS slab and calls this, so there is no separate share buffer and no host copy of Q0. */
+int cda_extend_commit_eds(cda_ctx* ctx, uint32_t k, uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots,
+                          uint8_t* dah, cda_err_info* err);
+
 /* Host buffers are streamed through the GPU in chunks: H2D of chunk i+1, the extension and trees
  * of chunk i and D2H of chunk i-1 overlap on three streams (PCIe full duplex).  Pageable memory
  * works; memory from cda_host_alloc (pinned) avoids the runtime's staging copies. */

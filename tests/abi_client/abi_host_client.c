@@ -204,6 +204,31 @@ int main(int argc, char** argv) {
   rc = cda_extend_commit(ctx, count, (uint32_t)S, ods, eds, rows, cols, dah, &err);
   if (rc) return fail("cda_extend_commit", rc, &err);
 
+  /* go/cda ExtendShares' call: the shares flattened into Q0 of a page-locked EDS buffer, extended in place
+     (cda_host_register, cda_extend_commit_eds); the same square, roots and DAH */
+  {
+    uint8_t* ip = malloc((size_t)w * w * S);
+    memset(ip, 0xC3, (size_t)w * w * S);
+    for (uint32_t r = 0; r < k; r++) memcpy(ip + (size_t)r * w * S, ods + (size_t)r * k * S, (size_t)k * S);
+    rc = cda_host_register(ctx, ip, (size_t)w * w * S);
+    if (rc) return fail("cda_host_register", rc, NULL);
+    uint8_t* r2 = malloc((size_t)w * CDA_NODE_SIZE);
+    uint8_t* c2 = malloc((size_t)w * CDA_NODE_SIZE);
+    uint8_t d2[32];
+    rc = cda_extend_commit_eds(ctx, k, ip, r2, c2, d2, &err);
+    if (rc) return fail("cda_extend_commit_eds", rc, &err);
+    if (memcmp(ip, eds, (size_t)w * w * S) || memcmp(r2, rows, (size_t)w * CDA_NODE_SIZE) ||
+        memcmp(c2, cols, (size_t)w * CDA_NODE_SIZE) || memcmp(d2, dah, 32)) {
+      fprintf(stderr, "cda_extend_commit_eds differs from cda_extend_commit\n");
+      return 1;
+    }
+    rc = cda_host_unregister(ctx, ip);
+    if (rc) return fail("cda_host_unregister", rc, NULL);
+    free(ip);
+    free(r2);
+    free(c2);
+  }
+
   /* rsmt2d.Codec.Encode of ODS row 0 (the same bytes as EDS row 0, columns k..2k-1) */
   uint8_t* parity = malloc((size_t)k * S);
   rc = cda_rs_encode(ctx, k, (uint32_t)S, ods, parity);

@@ -220,3 +220,91 @@ def test_one_block_copy_pool_fault_is_a_return_code(monkeypatch):
         _check(ods, eds, rr, cr, dah)
     finally:
         c.close()
+
+
+def _inplace_buffer(ods, k, fill=None):
+    """A (4k^2, 512) EDS buffer with the ODS in Q0 (what go/cda's ExtendShares flattens into its pooled slab)."""
+    eds = np.empty((4 * k * k, 512), np.uint8) if fill is None else np.full((4 * k * k, 512), fill, np.uint8)
+    eds.reshape(2 * k, 2 * k, 512)[:k, :k] = ods.reshape(k, k, 512)
+    return eds
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128, 256, 512])
+def test_extend_commit_eds_in_place(ctx, k):
+    """cda_extend_commit_eds: Q0 of the caller's buffer holds the ODS; Q1..Q3 written around it, bit-exact with the
+    oracle (k <= 256: the consensus path without its Q0 copy, 2-D input DMAs; k = 512: the gathered fallback).  The
+    rest of the buffer starts as other bytes, so every byte outside Q0 must be written."""
+    ods = O.gen_ods(k, 0x1D0 + k)
+    eds = _inplace_buffer(ods, k, fill=0xA5)
+    rr, cr, dah = ctx.extend_commit_eds(eds)
+    _check(ods, eds, rr, cr, dah)
+
+
+@pytest.mark.parametrize("kind", ["registered", "pinned", "fresh_tail", "written"])
+def test_extend_commit_eds_buffer_kinds(ctx, kind):
+    """The in-place form on every kind of caller buffer at k = 128: registered once and reused (go/cda's EDS pool,
+    several squares in a row), cda_host_alloc, a fresh buffer whose only written pages are Q0's, a written one."""
+    k = 128
+    seeds = (0x2A1, 0x2A2, 0x2A3)
+    if kind == "registered":
+        buf = np.full((4 * k * k, 512), 0x11, np.uint8)
+        ctx.host_register(buf)
+        try:
+            for seed in seeds:
+                ods = O.gen_ods(k, seed)
+                buf.reshape(2 * k, 2 * k, 512)[:k, :k] = ods.reshape(k, k, 512)
+                rr, cr, dah = ctx.extend_commit_eds(buf)
+                _check(ods, buf, rr, cr, dah)
+        finally:
+            ctx.host_unregister(buf)
+        return
+    if kind == "pinned":
+        p = ctx.pinned((4 * k * k, 512))
+        try:
+            ods = O.gen_ods(k, seeds[0])
+            p.array[:] = 0x22
+            p.array.reshape(2 * k, 2 * k, 512)[:k, :k] = ods.reshape(k, k, 512)
+            rr, cr, dah = ctx.extend_commit_eds(p.array)
+            _check(ods, p.array, rr, cr, dah)
+        finally:
+            p.free()
+        return
+    ods = O.gen_ods(k, seeds[1])
+    eds = _inplace_buffer(ods, k, fill=None if kind == "fresh_tail" else 0x33)
+    rr, cr, dah = ctx.extend_commit_eds(eds)
+    _check(ods, eds, rr, cr, dah)
+
+
+def test_extend_commit_eds_matches_extend_commit(ctx, serial_ctx):
+    """Same roots and DAH as cda_extend_commit on the same shares, on the consensus context and on a serial one (the
+    gathered fallback), and the same namespace push-order error."""
+    import cda
+    k = 64
+    ods = O.gen_ods(k, 0x3B3)
+    want = ctx.extend_commit(ods)
+    for c in (ctx, serial_ctx):
+        eds = _inplace_buffer(ods, k)
+        rr, cr, dah = c.extend_commit_eds(eds)
+        assert np.array_equal(eds, want[0].reshape(eds.shape))
+        assert np.array_equal(rr, want[1]) and np.array_equal(cr, want[2]) and bytes(dah) == bytes(want[3])
+    bad = ods.copy()
+    bad[[5, 6]] = bad[[6, 5]]
+    errs = []
+    for c in (ctx, serial_ctx):
+        with pytest.raises(cda.CdaError) as ei:
+            c.extend_commit_eds(_inplace_buffer(bad, k))
+        errs.append((ei.value.code, ei.value.axis, ei.value.index, ei.value.leaf))
+    with pytest.raises(cda.CdaError) as ei:
+        ctx.extend_commit(bad)
+    assert errs[0] == errs[1] == (ei.value.code, ei.value.axis, ei.value.index, ei.value.leaf)
+
+
+def test_extend_commit_eds_rejects_bad_shapes(ctx):
+    with pytest.raises(ValueError):
+        ctx.extend_commit_eds(np.zeros((3 * 3, 512), np.uint8))
+    with pytest.raises(ValueError):
+        ctx.extend_commit_eds(np.zeros((16, 256), np.uint8))
+    with pytest.raises(ValueError):
+        ctx.extend_commit_eds(np.zeros((16, 512), np.int8))
+    with pytest.raises(ValueError):
+        ctx.extend_commit_eds(np.zeros((16, 1024), np.uint8)[:, ::2])
