@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "cda.h"
 
@@ -371,5 +372,16 @@ int main(int argc, char** argv) {
   cda_free(ctx);
   free(ods); free(eds); free(rows); free(cols); free(parity); free(damaged); free(present);
   free(ods3); free(rows3); free(cols3); free(cw); free(cw_present);
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+  /* The AddressSanitizer build (make asan) leaves without the HIP runtime's exit-time teardown: there the ASan
+     runtime's interception of HSA memory trips its own CHECK ("dev_runtime_unloaded_", inside libhsa-runtime64's
+     destructors, after every libcda call has returned and cda_free has run) -- a sanitizer / runtime interaction,
+     not a libcda access. */
+  fflush(stdout);
+  fflush(stderr);
+  _exit(0);
+#endif
+#endif
   return 0;
 }

@@ -13,7 +13,8 @@ import pytest
 import oracle_lib as O
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CLIENT = os.path.join(HERE, "abi_client", "abi_host_client")
+# CDA_ABI_CLIENT: another build of the client (scripts/gpu_asan.sh runs these tests with the AddressSanitizer one)
+CLIENT = os.environ.get("CDA_ABI_CLIENT") or os.path.join(HERE, "abi_client", "abi_host_client")
 
 
 def test_client_is_built():
