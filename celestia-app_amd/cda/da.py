@@ -32,14 +32,38 @@ def is_power_of_two(n):
 
 
 def extend_shares(shares, codec=None):
-    """ExtendShares (:65-75)."""
+    """ExtendShares (:65-75).  As go/cda's ExtendSharesOn: a square of 512-byte shares is written straight into Q0 of
+    the EDS buffer and extended in place (cda_extend_commit_eds); anything else goes through cda_extend_commit, which
+    raises the reference's errors in its order (not a square, chunk size)."""
     if not is_power_of_two(len(shares)):
         raise DAError(f"number of shares is not a power of 2: got {len(shares)}")
     codec = codec or LeoRSCodec()
+    k = square_size(len(shares))
+    if k * k == len(shares) and all(len(s) == appconsts.SHARE_SIZE for s in shares):
+        eds = np.empty((4 * k * k, appconsts.SHARE_SIZE), np.uint8)
+        q0 = eds.reshape(2 * k, 2 * k, appconsts.SHARE_SIZE)[:k, :k]
+        for i, s in enumerate(shares):
+            q0[i // k, i % k] = np.frombuffer(bytes(s), np.uint8)
+        rr, cr, _ = codec.ctx.extend_commit_eds(eds)
+        return ExtendedDataSquare(eds, 2 * k, k, codec, rr, cr)
     arr = np.stack([np.frombuffer(bytes(s), np.uint8) for s in shares])
     eds, rr, cr, _ = codec.ctx.extend_commit(arr)
     k = int(round(len(shares) ** 0.5))
     return ExtendedDataSquare(eds, 2 * k, k, codec, rr, cr)
+
+
+def new_data_availability_header_from_shares(shares, ctx=None):
+    """NewDataAvailabilityHeaderFromShares (go/patches/0004: PrepareProposal / ProcessProposal read only the header,
+    app/prepare_proposal.go:65-93, app/process_proposal.go:137-151) = NewDataAvailabilityHeader(ExtendShares(s)) with
+    the same roots, hash and errors, from one cda_extend_commit that copies no EDS back."""
+    if not is_power_of_two(len(shares)):
+        raise DAError(f"number of shares is not a power of 2: got {len(shares)}")
+    ctx = ctx or N.default_context()
+    arr = np.stack([np.frombuffer(bytes(s), np.uint8) for s in shares])
+    _, rr, cr, h = ctx.extend_commit(arr, want_eds=False)
+    dah = DataAvailabilityHeader(list(rr), list(cr), ctx=ctx)
+    dah._hash = h
+    return dah
 
 
 class DataAvailabilityHeader:

@@ -29,6 +29,28 @@ def test_new_data_availability_header(ctx, k, expected):
     assert got.hash() == expected
 
 
+@pytest.mark.parametrize("k,expected", [(1, None), (2, kat.TYPICAL_K2), (128, kat.MAX_K128)])
+def test_dah_from_shares_roots_only(ctx, k, expected):
+    """go/patches/0004's NewDataAvailabilityHeaderFromShares (mirror: da.new_data_availability_header_from_shares):
+    the same roots and hash as NewDataAvailabilityHeader(ExtendShares(s)), which itself now extends in place."""
+    from cda import da
+    shares = da.min_shares() if k == 1 else [bytes(s) for s in kat.generate_shares(k * k)]
+    full = da.new_data_availability_header(da.extend_shares(shares))
+    fast = da.new_data_availability_header_from_shares(shares, ctx=ctx)
+    assert fast.row_roots == full.row_roots and fast.column_roots == full.column_roots
+    assert fast.hash() == full.hash() == (expected if expected is not None else kat.MIN_DAH)
+    fast.validate_basic()
+
+
+@pytest.mark.parametrize("count", [5, 8, 129 * 129])
+def test_dah_from_shares_errors(ctx, count):
+    from cda import da
+    with pytest.raises(Exception):
+        da.new_data_availability_header_from_shares([bytes(s) for s in kat.generate_shares(count)], ctx=ctx)
+    with pytest.raises(Exception):
+        da.extend_shares([bytes(s) for s in kat.generate_shares(count)])
+
+
 def test_nil_dah_hash(ctx):
     from cda import da
     assert da.DataAvailabilityHeader().hash() == kat.EMPTY_HASH
