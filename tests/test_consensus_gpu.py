@@ -308,3 +308,53 @@ def test_extend_commit_eds_rejects_bad_shapes(ctx):
         ctx.extend_commit_eds(np.zeros((16, 512), np.int8))
     with pytest.raises(ValueError):
         ctx.extend_commit_eds(np.zeros((16, 1024), np.uint8)[:, ::2])
+
+
+def test_extend_commit_eds_concurrent_callers(ctx):
+    """In-place calls from several host threads on one context, mixed with roots-only calls (the consensus handlers
+    and ExtendBlock of one node): every square and DAH exact."""
+    k = 64
+    odss = [O.gen_ods(k, 0x5100 + i) for i in range(4)]
+    want = [O.extend_commit(o) for o in odss]
+    errs = []
+
+    def run(i):
+        try:
+            for it in range(3):
+                if (i + it) % 2:
+                    eds = _inplace_buffer(odss[i], k)
+                    rr, cr, dah = ctx.extend_commit_eds(eds)
+                    assert np.array_equal(eds, want[i][1].reshape(eds.shape)) and dah == want[i][4]
+                else:
+                    assert ctx.extend_commit(odss[i], want_eds=False)[3] == want[i][4]
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(odss))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+
+
+def test_extend_commit_eds_copy_pool_fault_is_a_return_code(monkeypatch):
+    """In place with the copy pool's threads failing to start (test-hooks build): CDA_E_INTERNAL, the buffer's Q0 is
+    untouched, and the next in-place call on the context is exact."""
+    import cda
+    from cda import _native as N
+    c = cda.Context(0, lib_path=N.HOOKS_LIB_PATH)
+    try:
+        k = 32
+        ods = O.gen_ods(k, 0x5200)
+        eds = _inplace_buffer(ods, k, fill=0x44)
+        monkeypatch.setenv("CDA_FAULT_INJECT", "thread")
+        with pytest.raises(cda.CdaError) as ei:
+            c.extend_commit_eds(eds)
+        assert ei.value.code == N.E_INTERNAL
+        assert np.array_equal(eds.reshape(2 * k, 2 * k, 512)[:k, :k], ods.reshape(k, k, 512))
+        monkeypatch.delenv("CDA_FAULT_INJECT")
+        rr, cr, dah = c.extend_commit_eds(eds)
+        _check(ods, eds, rr, cr, dah)
+    finally:
+        c.close()
