@@ -103,6 +103,7 @@ def test_release_library_ignores_fault_injection(monkeypatch):
         assert L.cda_extend_commit(None, 4, 512, None, None, None, None, None, None) == N.E_ARG
         assert L.cda_set_option(None, N.OPT_HUGE_PAGES, 1) == N.E_ARG
         assert L.cda_host_register(None, None, 0) == N.E_ARG
+        assert L.cda_extend_commit_eds(None, 8, None, None, None, None, None) == N.E_ARG
 
 
 def test_release_library_reads_no_environment_per_call():
