@@ -885,6 +885,8 @@ __device__ __forceinline__ void body2(const Args& a, uint4* xb, int w) {
 __global__ void __launch_bounds__(1024, 1) rs_encode16_reg_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint4 xb[];  // 64 keys x 2 quads x 64 lanes x 16 B = 128 KiB
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // (s_setprio 1 for waves 8-15, so that the second-dispatched half does not lose every issue arbitration before the
+  // exchange barriers: columns 0.250-0.260 vs 0.252-0.258 ms per square, profiles/r05_prio_ab.log; not kept)
 #if CDA_RS16_PIPE && CDA_RS16_DIAG_MODE == 0
 #define CDA_RS16_BODY body2
 #else

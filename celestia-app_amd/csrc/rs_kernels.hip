@@ -534,6 +534,8 @@ __global__ void __launch_bounds__(64 << (L - 4), 4) rs_encode8_g2_kernel(Rs8RegA
   // x, x + 8, ...; map them to one contiguous range of codeword pairs per XCD
   const unsigned g = gridDim.x, b = blockIdx.x;
   const int wg = (a.remap && (g % 8u) == 0) ? (int)((b % 8u) * (g / 8u) + b / 8u) : (int)b;
+  // (static issue priority, s_setprio 1, for the second half of the waves: columns 0.857 vs 0.839 ms per B = 128
+  // step in a rotating same-box A/B, profiles/r05_prio_ab.log; not kept)
   rs_g2_body<L>(a, wg, xbuf);
 }
 
