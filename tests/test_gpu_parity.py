@@ -51,6 +51,40 @@ def test_dah_from_shares_errors(ctx, count):
         da.extend_shares([bytes(s) for s in kat.generate_shares(count)])
 
 
+def test_dah_validate_basic_cases(ctx):
+    """Test_DAHValidateBasic (pkg/da/data_availability_header_test.go:135-215): min and max headers pass; too many
+    roots, too few roots, a wrong hash and unequal root counts fail with the reference's messages."""
+    from cda import appconsts, da
+    max_size = appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND ** 2
+    big = da.new_data_availability_header(da.extend_shares([bytes(s) for s in kat.generate_shares(max_size)]))
+    too_big = da.DataAvailabilityHeader(big.row_roots + [b"\x00"] * (max_size - len(big.row_roots)) + [b"\x01" * 32],
+                                        big.column_roots + [b"\x00"] * (max_size - len(big.column_roots)) +
+                                        [b"\x01" * 32], ctx=ctx)
+    too_small = da.DataAvailabilityHeader([b"\x02" * 32], [b"\x02" * 32], ctx=ctx)
+    bad_hash = da.min_data_availability_header()
+    bad_hash._hash = bytes([1, 2, 3, 4])
+    mismatch = da.min_data_availability_header()
+    mismatch.column_roots.append(b"\x02" * 32)
+    da.min_data_availability_header().validate_basic()
+    big.validate_basic()
+    for dah, msg in ((too_big, "maximum valid DataAvailabilityHeader has at most"),
+                     (too_small, "minimum valid DataAvailabilityHeader has at least"),
+                     (bad_hash, "wrong hash"),
+                     (mismatch, "unequal number of row and column roots")):
+        with pytest.raises(da.DAError) as ei:
+            dah.validate_basic()
+        assert msg in str(ei.value), (msg, str(ei.value))
+
+
+def test_dah_square_size(ctx):
+    """TestSquareSize (data_availability_header_test.go:217-240): 1 for the min header, the upper bound for the max."""
+    from cda import appconsts, da
+    assert da.min_data_availability_header().square_size() == 1
+    n = appconsts.DEFAULT_SQUARE_SIZE_UPPER_BOUND
+    big = da.new_data_availability_header(da.extend_shares([bytes(s) for s in kat.generate_shares(n * n)]))
+    assert big.square_size() == n
+
+
 def test_nil_dah_hash(ctx):
     from cda import da
     assert da.DataAvailabilityHeader().hash() == kat.EMPTY_HASH

@@ -103,8 +103,10 @@ def test_get_commitment_random_vs_oracle(ctx, k):
 
 
 @pytest.mark.parametrize("k,ranges", [(1, [(0, 1)]), (4, [(0, 1), (0, 16), (3, 9), (5, 6), (15, 16)]),
-                                      (16, [(0, 53), (17, 200), (255, 256), (16, 32)])])
+                                      (16, [(0, 53), (17, 200), (255, 256), (16, 32), (0, 256)])])
 def test_share_inclusion_proof_vs_oracle(ctx, k, ranges):
+    """Row / NMT range proofs of ODS share ranges vs the oracle; (0, 256) at k = 16 is TestAllSharesInclusionProof's
+    whole 256-share square (pkg/proof/proof_test.go:234-262)."""
     ods = O.gen_ods(k, 0xF00D + k)
     eds = O.extend(ods)
     rc, rr, cr, *_ = O.roots(eds)
