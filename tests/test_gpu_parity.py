@@ -305,6 +305,42 @@ def test_wrapper_tree_roots(ctx):
         assert t.root() == bytes(rr[r])
 
 
+def _erasured_data(k, seed, codec):
+    """generateErasuredData (nmt_wrapper_test.go:139-149): k random namespaced shares, sorted, then Codec.Encode."""
+    raw = [bytes(s) for s in O.gen_ods(k, seed)[:k]]
+    raw.sort()
+    return raw + codec.encode(raw)
+
+
+@pytest.mark.parametrize("k", [8, 128])
+def test_push_erasured_data(ctx, k):
+    """TestPushErasuredNamespacedMerkleTree (nmt_wrapper_test.go:19-42): 2k pushes of data + parity succeed, and the
+    root equals the oracle's axis root of the same leaves (axis 0: the first k leaves keep their namespaces)."""
+    from cda.rsmt2d import LeoRSCodec
+    from cda.wrapper import ErasuredNamespacedMerkleTree
+    data = _erasured_data(k, 0x77 + k, LeoRSCodec(ctx))
+    t = ErasuredNamespacedMerkleTree(k, 0, ctx)
+    for d in data:
+        t.push(d)
+    rc, want, _ = O.nmt_axis_root(k, 0, data)
+    assert rc == 0 and t.root() == want
+
+
+def test_push_errors_with_erasured_data(ctx):
+    """TestErasureNamespacedMerkleTreePushErrors (nmt_wrapper_test.go:91-128), k = 16: pushing the erasured data of
+    k + 1 shares, the erasured data in reverse order, or a 1-byte share fails."""
+    from cda.rsmt2d import LeoRSCodec
+    from cda.wrapper import ErasuredNamespacedMerkleTree, PushError
+    codec = LeoRSCodec(ctx)
+    over = _erasured_data(17, 0x91, codec)
+    rev = sorted(_erasured_data(16, 0x92, codec), reverse=True)
+    for data in (over, rev, [b"\x01"]):
+        t = ErasuredNamespacedMerkleTree(16, 0, ctx)
+        with pytest.raises(PushError):
+            for d in data:
+                t.push(d)
+
+
 def test_empty_tree_root(ctx):
     from cda.wrapper import ErasuredNamespacedMerkleTree
     r1 = ErasuredNamespacedMerkleTree(1, 0, ctx).root()
