@@ -89,6 +89,19 @@ def test_get_commitment_mainnet(ctx):
         assert I.get_commitment(cacher, dah, b["start"], b["n"], 64, ctx=ctx) == b["commitment"]
 
 
+def test_eds_sub_root_cacher(ctx):
+    """TestEDSSubRootCacher (pkg/inclusion/nmt_caching_test.go:117-138), k = 8: for every ODS row, the subtree root
+    three steps left of the row root is the NMT root of the row's first two shares pushed into a fresh tree (their
+    own namespaces: quadrant zero)."""
+    from cda import inclusion as I
+    k = 8
+    ods = O.gen_ods(k, 0xCAC4E)
+    cacher, dah = I.EDSSubTreeRootCacher.from_shares([bytes(s) for s in ods], ctx=ctx)
+    for i in range(k):
+        rc, want, _ = O.nmt_axis_root(k, 0, [bytes(ods[i * k]), bytes(ods[i * k + 1])])
+        assert rc == 0 and cacher.get_sub_tree_root(dah, i, [False, False, False]) == want, i
+
+
 @pytest.mark.parametrize("k", [4, 16])
 def test_get_commitment_random_vs_oracle(ctx, k):
     from cda import inclusion as I
