@@ -181,3 +181,28 @@ def test_oracle_merkle_proofs(n):
         assert root == want_root
         assert O.merkle_verify(n, i, leaf, aunts, root, items[i])
         assert not O.merkle_verify(n, i, leaf, aunts, root, items[(i + 1) % n]) or n == 1
+
+
+@pytest.mark.parametrize("start,end,msg", [(-1, 1, "should be positive"), (0, -1, "should be positive"),
+                                           (10, 9, "cannot be lower than starting share"),
+                                           (0, 1025, "is higher than block shares")])
+def test_parse_namespace_rejects_bad_ranges(start, end, msg):
+    """TestNewShareInclusionProof's error cases (pkg/proof/proof_test.go:98-232; querier.go ParseNamespace) on
+    mainnet block 408's 32 x 32 square: negative start / end, end below start, end past the square's 1,024 shares;
+    and a range spanning two namespaces."""
+    from cda import proof as P
+    shares = [bytes(s) for s in mainnet_ods()]
+    with pytest.raises(P.ProofError) as ei:
+        P.parse_namespace(shares, start, end)
+    assert msg in str(ei.value)
+
+
+def test_parse_namespace_single_namespace_ranges():
+    from cda import proof as P
+    shares = [bytes(s) for s in mainnet_ods()]
+    b = mainnet_blobs()[0]
+    assert P.parse_namespace(shares, 0, 1) == shares[0][:29]
+    assert P.parse_namespace(shares, b["start"], b["start"] + b["n"]) == shares[b["start"]][:29]
+    with pytest.raises(P.ProofError) as ei:
+        P.parse_namespace(shares, b["start"] - 1, b["start"] + 1)
+    assert "different namespaces" in str(ei.value)
