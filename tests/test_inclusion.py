@@ -206,3 +206,82 @@ def test_parse_namespace_single_namespace_ranges():
     with pytest.raises(P.ProofError) as ei:
         P.parse_namespace(shares, b["start"] - 1, b["start"] + 1)
     assert "different namespaces" in str(ei.value)
+
+
+# ---- pkg/proof Validate mirrors (cda.proof), on the reference's own fixtures ---------------------------------------
+def _fixture_proofs():
+    from cda import proof as P
+    fx = _fixture()
+    p = fx["row_proof"]
+    pr = P.Proof(p["total"], p["index"], bytes.fromhex(p["leaf_hash"]), [bytes.fromhex(a) for a in p["aunts"]])
+    rp = P.RowProof([bytes.fromhex(r) for r in fx["row_roots"]], [pr], fx["start_row"], fx["end_row"])
+    nm = P.NMTProof(fx["nmt"]["start"], fx["nmt"]["end"], [bytes.fromhex(x) for x in fx["nmt"]["nodes"]])
+    sp = P.ShareProof([bytes.fromhex(d) for d in fx["data"]], [nm], bytes.fromhex(fx["namespace_id"]), rp,
+                      fx["namespace_version"])
+    return bytes.fromhex(fx["root"]), rp, sp
+
+
+def test_row_proof_validate_cases():
+    """TestRowProofValidate (pkg/proof/row_proof_test.go:10-66) on its own vector."""
+    import copy
+    from cda import proof as P
+    root, rp, _ = _fixture_proofs()
+    rp.validate(root)  # "valid row proof returns no error"
+    cases = {"empty": P.RowProof([], [], 0, 0)}
+    cases["mismatched row roots"] = copy.deepcopy(rp)
+    cases["mismatched row roots"].row_roots = []
+    cases["mismatched proofs"] = copy.deepcopy(rp)
+    cases["mismatched proofs"].proofs = []
+    cases["mismatched rows"] = copy.deepcopy(rp)
+    cases["mismatched rows"].end_row = 10
+    for name, bad in cases.items():
+        with pytest.raises(P.ProofError):
+            bad.validate(root)
+    with pytest.raises(P.ProofError):  # "valid row proof with incorrect root"
+        rp.validate(bytes(32))
+
+
+def test_share_proof_validate_cases():
+    """TestShareProofValidate (pkg/proof/share_proof_test.go:9-60) on its own vector (33-byte namespace)."""
+    import copy
+    from cda import proof as P
+    root, _, sp = _fixture_proofs()
+    sp.validate(root)
+    empty = P.ShareProof(None, [], b"", P.RowProof([], [], 0, 0), 0)
+    fewer_proofs = copy.deepcopy(sp)
+    fewer_proofs.share_proofs = []
+    more_shares = copy.deepcopy(sp)
+    more_shares.data = more_shares.data + [more_shares.data[0]]
+    for bad in (empty, fewer_proofs, more_shares):
+        with pytest.raises(P.ProofError):
+            bad.validate(root)
+    with pytest.raises(P.ProofError):
+        sp.validate(bytes(32))
+    tampered = copy.deepcopy(sp)
+    d = bytearray(tampered.data[0])
+    d[100] ^= 1
+    tampered.data[0] = bytes(d)
+    assert not tampered.verify_proof()
+
+
+@pytest.mark.parametrize("k", [1, 2, 4])
+def test_nmt_verify_inclusion_matches_oracle(k):
+    """cda.proof's NMT inclusion verifier agrees with the oracle's on every single-namespace range of real erasured
+    rows (ranges proved by the oracle's ProveRange), and rejects a proof with a node dropped."""
+    from cda import proof as P
+    eds = O.extend(O.gen_ods(k, 71 + k))
+    rc, rr, *_ = O.roots(eds)
+    w = 2 * k
+    for row in {0, w - 1}:
+        leaves = O.axis_leaf_nodes(eds, 0, row)
+        cells = eds.reshape(w, w, 512)[row]
+        for s in range(w):
+            for e in range(s + 1, w + 1):
+                ns = leaves[s][:29].tobytes()
+                if any(leaves[i][:29].tobytes() != ns for i in range(s, e)):
+                    continue
+                nodes = O.nmt_prove_range(leaves, s, e)
+                data = [cells[i].tobytes() for i in range(s, e)]
+                assert P.NMTProof(s, e, nodes).verify_inclusion(ns, data, rr[row].tobytes())
+                if nodes:
+                    assert not P.NMTProof(s, e, nodes[:-1]).verify_inclusion(ns, data, rr[row].tobytes())

@@ -157,6 +157,9 @@ def test_share_inclusion_proof_mainnet_verifies(ctx):
             assert O.nmt_verify_inclusion(ns, sp.data[cursor:cursor + used], nm.start, nm.end, nm.nodes, rr)
             cursor += used
         assert cursor == end - start
+        sp.validate(data_hash)  # ShareProof.Validate (cda.proof mirror) on the GPU-built proof
+        with pytest.raises(P.ProofError):
+            sp.validate(bytes(32))
     with pytest.raises(P.ProofError):
         P.parse_namespace(shares, 0, b["start"] + 1)  # spans several namespaces
 
