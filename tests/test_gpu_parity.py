@@ -341,6 +341,27 @@ def test_push_errors_with_erasured_data(ctx):
                 t.push(d)
 
 
+def test_erasured_tree_prove_range(ctx):
+    """TestErasuredNamespacedMerkleTree_ProveRange (nmt_wrapper_test.go:152-182): for square sizes 1..16, the
+    single-share proofs of every leaf of a tree of codec-erasured data are non-empty and verify against the tree's
+    (GPU) root, under the share's namespace for i < k and the parity namespace above."""
+    from cda.appconsts import PARITY_SHARES_NAMESPACE
+    from cda.rsmt2d import LeoRSCodec
+    from cda.wrapper import ErasuredNamespacedMerkleTree
+    codec = LeoRSCodec(ctx)
+    for k in range(1, 17):
+        data = _erasured_data(k, 0x600 + k, codec)
+        t = ErasuredNamespacedMerkleTree(k, 0, ctx)
+        for d in data:
+            t.push(d)
+        root = t.root()
+        for i in range(len(data)):
+            p = t.prove_range(i, i + 1)
+            assert p.nodes, (k, i)
+            ns = data[i][:29] if i < k else PARITY_SHARES_NAMESPACE
+            assert p.verify_inclusion(ns, [data[i]], root), (k, i)
+
+
 def test_empty_tree_root(ctx):
     from cda.wrapper import ErasuredNamespacedMerkleTree
     r1 = ErasuredNamespacedMerkleTree(1, 0, ctx).root()

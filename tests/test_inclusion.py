@@ -285,3 +285,28 @@ def test_nmt_verify_inclusion_matches_oracle(k):
                 assert P.NMTProof(s, e, nodes).verify_inclusion(ns, data, rr[row].tobytes())
                 if nodes:
                     assert not P.NMTProof(s, e, nodes[:-1]).verify_inclusion(ns, data, rr[row].tobytes())
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8])
+def test_wrapper_prove_range_matches_oracle(k):
+    """wrapper ErasuredNamespacedMerkleTree.ProveRange (host, cda.wrapper) gives the oracle's proof nodes for every
+    range of real erasured rows and columns, and each proof verifies against the oracle's root (cda.proof)."""
+    from cda.wrapper import ErasuredNamespacedMerkleTree
+    eds = O.extend(O.gen_ods(k, 91 + k))
+    rc, rr, cr, *_ = O.roots(eds)
+    w = 2 * k
+    sq = eds.reshape(w, w, 512)
+    for axis, idx in ((0, 0), (0, w - 1), (1, 0), (1, k)):
+        cells = sq[idx] if axis == 0 else sq[:, idx]
+        root = (rr if axis == 0 else cr)[idx].tobytes()
+        leaves = O.axis_leaf_nodes(eds, axis, idx)
+        t = ErasuredNamespacedMerkleTree(k, idx)
+        for c in cells:
+            t.push(c.tobytes())
+        for s in range(w):
+            for e in range(s + 1, w + 1):
+                p = t.prove_range(s, e)
+                assert p.nodes == O.nmt_prove_range(leaves, s, e), (axis, idx, s, e)
+                ns = leaves[s][:29].tobytes()
+                if all(leaves[i][:29].tobytes() == ns for i in range(s, e)):
+                    assert p.verify_inclusion(ns, [cells[i].tobytes() for i in range(s, e)], root)
