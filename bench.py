@@ -771,7 +771,9 @@ def one_block_fresh(ctx, ods, reps=25, warmup=3):
         pb_ods.free()
         pb_eds.free()
     res["consensus_targets_ms"] = {"roots_only_median": 0.45, "pooled_eds_median": 0.70,
-                                   "source": "VERDICT r04 next #1 (driver BENCH line)"}
+                                   "source": "VERDICT r04 next #1 (driver BENCH line)",
+                                   "go_calls": {"PrepareProposal/ProcessProposal (patch 0004)": "roots_only",
+                                                "ExtendShares/ExtendBlock (go/cda/pool.go)": "pooled_eds_inplace"}}
     res["note"] = (f"cda_extend_commit_batch, one k={k} block per call, {warmup} untimed + {reps} timed calls per "
                    f"series; csrc/consensus.cpp; pooled slabs: np.empty + cda_host_register, two per pool, "
                    f"round-robin (go/cda/pool.go)")
