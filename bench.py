@@ -263,12 +263,101 @@ def cpu_baseline(k, seconds, gpu=None):
             raise RuntimeError("GPU blob commitment differs from the CPU restatement's")
         n_cpu += 1
     out["blob_commitments_1thread_per_s"] = round(n_cpu / (time.perf_counter() - t0), 1)
+    # the per-axis shapes (rsmt2d over the CPU codec and wrapper tree) on the restatement, beside result["per_axis"]
+    try:
+        out["per_axis"] = per_axis_measure("oracle", os.path.join(ROOT, "oracle", "liboracle.so"), reps=3,
+                                           reps_repair=2, reps_single=100)
+    except Exception as e:
+        out["per_axis"] = {"error": f"{type(e).__name__}: {e}"}
     out["sample"] = (f"k={k} ExtendShares+NewDataAvailabilityHeader (EDS written) via oracle/liboracle.so (C "
                      f"restatement, OpenSSL SHA-256 (SHA-NI), AVX2 Leopard; not the Go reference): throughput = "
                      f"independent blocks, one single-threaded call per worker thread, {seconds / len(counts):.1f} s "
                      f"per thread count over 1..{allt} threads (cgroup quota {topo['cgroup_cpu_quota']} CPUs), "
                      f"(blocks, s) per count: {total_blocks}; single_block_ms / repair_c4_ms / k512_ms: best of 1-3 "
                      f"calls; blob commitments: 64 KiB blobs")
+    return out
+
+
+AXES_DRIVER = os.path.join(ROOT, "tests", "abi_client", "rsmt2d_axes")
+
+
+def _rfc6962_root(items):
+    import hashlib
+    if not items:
+        return hashlib.sha256(b"").digest()
+    if len(items) == 1:
+        return hashlib.sha256(b"\x00" + items[0]).digest()
+    s = 1
+    while s * 2 < len(items):
+        s *= 2
+    return hashlib.sha256(b"\x01" + _rfc6962_root(items[:s]) + _rfc6962_root(items[s:])).digest()
+
+
+def per_axis_measure(backend, lib_path, k=128, threads=8, reps_single=200, reps=5, reps_repair=5, seed=0xC0FFEE):
+    """The per-axis drop-in seams -- what rsmt2d reaches when it runs with appconsts.DefaultCodec = cda.NewCodec and
+    the GPU wrapper tree (go/pkg_da/extend_rocm.go): Codec.Encode / Decode (cda_rs_encode / cda_rs_decode) and the
+    tree Root (cda_nmt_axis_root, pkg/wrapper/nmt_wrapper.go:118-124), each call through pageable host buffers as cgo
+    passes Go slices.  tests/abi_client/rsmt2d_axes (a plain C caller, dlopen'ing `lib_path`) times:
+    * single: one Encode (k x 512 B), one Decode (2k shards, half present), one Root (2k leaves);
+    * extend: ComputeExtendedDataSquare + RowRoots/ColRoots in rsmt2d's shape -- erasureExtendSquare's 3k Encodes and
+      computeRoots' 4k Roots, one task per axis ("goroutine") on `threads` OS threads;
+    * repair_random / repair_q0_only: Repair in rsmt2d's shape (parallel prerepairSanityCheck, then the sequential
+      crossword: Decode + Root per axis, Roots of newly completed orthogonal axes) of config C4's squares.
+    backend "cda" = libcda (GPU), "oracle" = the CPU restatement (bench's cpu_baseline leg).  Every output is checked:
+    the extension's DAH against tests/golden/bench_digests.json, each repair against the full square."""
+    import subprocess
+    import tempfile
+    if not os.path.exists(AXES_DRIVER):
+        raise RuntimeError("tests/abi_client/rsmt2d_axes not built (__graft_entry__.build())")
+    w = 2 * k
+    tmp = tempfile.mkdtemp(prefix="per_axis_")
+    ods = gen_ods(k, seed).reshape(k * k, 512)
+    ods_p = os.path.join(tmp, "ods.bin")
+    ods.tofile(ods_p)
+
+    def run(*args, timeout=600):
+        p = subprocess.run([AXES_DRIVER, backend, lib_path] + [str(a) for a in args], capture_output=True, text=True,
+                           timeout=timeout)
+        if p.returncode != 0:
+            raise RuntimeError(f"rsmt2d_axes {args[0]} failed ({p.returncode}): {p.stderr.strip()[-400:]}")
+        return json.loads(p.stdout.strip().splitlines()[-1])
+
+    out = {"k": k, "threads": threads, "backend": backend}
+    out["single"] = run("single", k, reps_single, ods_p)
+    # as Go runs it: errgroup starts one goroutine per axis and each blocks in cgo on its own OS thread
+    out["extend_thread_per_axis"] = run("extend", k, 2 * k, reps, ods_p, tmp)
+    out["extend"] = ext = run("extend", k, threads, reps, ods_p, tmp)
+    eds = np.fromfile(os.path.join(tmp, "eds.bin"), np.uint8).reshape(w * w, 512)
+    rr = np.fromfile(os.path.join(tmp, "row_roots.bin"), np.uint8).reshape(w, 90)
+    cr = np.fromfile(os.path.join(tmp, "col_roots.bin"), np.uint8).reshape(w, 90)
+    dah = _rfc6962_root([bytes(r) for r in rr] + [bytes(c) for c in cr]).hex()
+    path = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+    want = json.load(open(path)).get(f"k{k}", {}).get(str(seed)) if os.path.exists(path) else None
+    if want is not None and dah != want:
+        raise RuntimeError(f"per-axis extension ({backend}) DAH {dah} != committed digest {want}")
+    ext["dah_checked_vs_golden"] = want is not None
+    roots_p = os.path.join(tmp, "roots.bin")
+    np.concatenate([rr, cr]).tofile(roots_p)
+    eds_p = os.path.join(tmp, "eds_full.bin")
+    eds.tofile(eds_p)
+    rng = np.random.default_rng(7)  # config C4's damaged squares (repair_measure / cpu_baseline: the same seed)
+    q0 = np.zeros((w, w), np.uint8)
+    q0[:k, :k] = 1
+    for name, pres in (("random", (rng.random(w * w) < 0.5).astype(np.uint8)), ("q0_only", q0.reshape(-1))):
+        pres_p = os.path.join(tmp, f"present_{name}.bin")
+        pres.tofile(pres_p)
+        r = run("repair", k, threads, reps_repair, eds_p, pres_p, roots_p, tmp)
+        rep = np.fromfile(os.path.join(tmp, "repaired.bin"), np.uint8).reshape(w * w, 512)
+        if r["rc"] != 0 or not np.array_equal(rep, eds):
+            raise RuntimeError(f"per-axis repair ({backend}, {name}) rc {r['rc']} did not restore the square")
+        out[f"repair_{name}"] = r
+    for f in os.listdir(tmp):
+        os.remove(os.path.join(tmp, f))
+    os.rmdir(tmp)
+    out["note"] = ("[min, median] over the timed calls; pageable malloc'd buffers (Go slices); extend/roots: one task per "
+                   "axis on `threads` OS threads (extend_thread_per_axis: one thread per task, as Go's errgroup "
+                   "goroutines each block in cgo on their own thread); repair: crossword sequential as in rsmt2d, the "
+                   "sanity check's axes in parallel")
     return out
 
 
@@ -1201,6 +1290,11 @@ def bench_main(args, world, rank, local, helper):
         result["share_proof"] = proof_measure(ctx, k)
         result["k512_single"] = k512_measure(ctx, dev)
         result["device_square"] = square_measure(ctx)
+        try:  # the per-axis seams (rsmt2d over cda.NewCodec + the GPU tree): VERDICT r05 next #1
+            from cda import _native
+            result["per_axis"] = per_axis_measure("cda", _native.LIB_PATH)
+        except Exception as e:  # reported, never the headline's exit code
+            result["per_axis"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cb = cpu_baseline(k, args.cpu_seconds, gpu)
         result["gpu_vs_cpu"] = gpu_vs_cpu(result, value)
@@ -1310,6 +1404,17 @@ def gpu_vs_cpu(result, value):
         if case in c4 and case in g4:
             out[f"repair_{case}_host_buffers"] = round(c4[case] / g4[case]["ms_median"], 1)
             out[f"repair_{case}_device_resident"] = round(c4[case] / g4[case]["device_resident_ms_median"], 1)
+    pa, pc = result.get("per_axis", {}), cb.get("per_axis", {})
+    if "single" in pa and "single" in pc:  # CPU median / GPU median per shape (> 1: the GPU seam is faster)
+        pv = {f"single_{op}": round(pc["single"][f"{op}_us"][1] / pa["single"][f"{op}_us"][1], 2)
+              for op in ("encode", "decode", "root")}
+        pv["extend_and_roots"] = round(pc["extend"]["total_ms"][1] / pa["extend"]["total_ms"][1], 2)
+        if "extend_thread_per_axis" in pa and "extend_thread_per_axis" in pc:
+            pv["extend_and_roots_thread_per_axis"] = round(pc["extend_thread_per_axis"]["total_ms"][1] /
+                                                           pa["extend_thread_per_axis"]["total_ms"][1], 2)
+        for case in ("random", "q0_only"):
+            pv[f"repair_{case}"] = round(pc[f"repair_{case}"]["repair_ms"][1] / pa[f"repair_{case}"]["repair_ms"][1], 2)
+        out["per_axis_cpu_over_gpu"] = pv
     k5 = cb.get("k512_ms", {})
     g5 = result.get("k512_single", {})
     if k5 and g5:

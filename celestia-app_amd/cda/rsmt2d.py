@@ -5,6 +5,8 @@ selected at pkg/appconsts/global_consts.go:92), ComputeExtendedDataSquare,
 ExtendedDataSquare.{RowRoots,ColRoots,Row,Col,GetCell,SetCell,Flattened,Width},
 Repair and its error types.  All arithmetic runs in libcda on the GPU.
 """
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 from . import _native as N
@@ -45,6 +47,8 @@ class LeoRSCodec:
     def decode(self, shards):
         """Codec.Decode: shards with None for missing -> all shards."""
         n = len(shards)
+        if not any(s is not None for s in shards):  # go/cda Codec.Decode: no shard to read a size from
+            raise N.CdaError(N.E_TOO_FEW)
         L = max(len(s) for s in shards if s is not None)
         arr = np.zeros((n, L), np.uint8)
         present = np.zeros(n, np.uint8)
@@ -160,6 +164,145 @@ def compute_extended_data_square(data, codec=None, tree_constructor=None):
     return sq
 
 
+
+
+def compute_extended_data_square_axes(data, codec=None, tree_constructor=None, workers=8):
+    """rsmt2d.ComputeExtendedDataSquare as upstream rsmt2d v0.12.0 runs it on an unpatched caller -- the shape every
+    rsmt2d user gets with appconsts.DefaultCodec = the GPU codec (go/pkg_da/extend_rocm.go): erasureExtendSquare
+    encodes one axis per task through codec.encode (row i then column i for i < k, then rows k..2k-1: Q3 = Enc(Q2
+    rows)), and computeRoots pushes each axis into a tree from `tree_constructor` (default wrapper.NewConstructor(k),
+    whose Root is cda_nmt_axis_root) and takes its Root, one task per index.  `workers` threads stand in for the
+    goroutines; concurrent calls meet in libcda's axis queue (axisq.cpp).  Same bytes as compute_extended_data_square,
+    which runs the whole square as one fused call."""
+    from . import wrapper
+    codec = codec or LeoRSCodec()
+    if len(data) > codec.max_chunks():
+        raise ValueError("number of chunks exceeds the maximum")
+    k = int(round(len(data) ** 0.5))
+    if k * k != len(data):
+        raise ValueError("number of chunks must be a square number")
+    w = 2 * k
+    L = len(bytes(data[0])) if k else 512
+    cells = np.zeros((w * w, L), np.uint8)
+    grid = cells.reshape(w, w, L)
+    for i, d in enumerate(data):
+        grid[i // k, i % k] = np.frombuffer(bytes(d), np.uint8)
+    tree_constructor = tree_constructor or wrapper.new_constructor(k, codec.ctx)
+
+    def extend_row(i):  # erasureExtendRow: Encode(rowSlice(i, 0, k)) -> setRowSlice(i, k, parity)
+        par = codec.encode([grid[i, j].tobytes() for j in range(k)])
+        for j, p in enumerate(par):
+            grid[i, k + j] = np.frombuffer(p, np.uint8)
+
+    def extend_col(i):  # erasureExtendCol: Encode(colSlice(0, i, k)) -> setColSlice(k, i, parity)
+        par = codec.encode([grid[j, i].tobytes() for j in range(k)])
+        for j, p in enumerate(par):
+            grid[k + j, i] = np.frombuffer(p, np.uint8)
+
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        list(ex.map(lambda i: (extend_row(i), extend_col(i)), range(k)))
+        list(ex.map(lambda i: extend_row(k + i), range(k)))
+        sq = ExtendedDataSquare(cells, w, k, codec)
+        roots = list(ex.map(lambda i: (_axis_root(sq, tree_constructor, ROW, i),
+                                       _axis_root(sq, tree_constructor, COL, i)), range(w)))
+    sq._row_roots = np.stack([np.frombuffer(r, np.uint8) for r, _ in roots])
+    sq._col_roots = np.stack([np.frombuffer(c, np.uint8) for _, c in roots])
+    return sq
+
+
+def _axis_root(sq, tree_constructor, axis, i, cells=None):
+    """rsmt2d computeSharesRoot: a fresh tree from the constructor, the axis's cells pushed in order, Root()."""
+    tree = tree_constructor(axis, i)
+    for share in (cells if cells is not None else (sq.row(i) if axis == ROW else sq.col(i))):
+        tree.push(share)
+    return bytes(tree.root())
+
+
+def repair_axes(sq, row_roots, col_roots, tree_constructor=None, workers=8):
+    """(*ExtendedDataSquare).Repair as upstream rsmt2d v0.12.0 runs it over the codec and tree seams -- what
+    celestia-node's Repair of a square returned by cda.ExtendShares reaches: prerepairSanityCheck (every complete
+    axis's root against the given roots and its parity against codec.encode of its data half, one task per axis),
+    then solveCrossword sequentially: for each index, row then column, an incomplete axis is rebuilt with codec.decode
+    when it can be, its root checked, the roots of the orthogonal axes it completes checked, and its cells set; sweeps
+    repeat until the square is complete (ok) or a sweep makes no progress (ErrUnrepairableDataSquare).  A mismatch
+    raises ErrByzantineData(axis, index) with the square left as repaired so far.  Same result as sq.repair (one
+    cda_repair call), one device round trip per axis instead."""
+    from . import wrapper
+    w, k = sq.width(), sq.original_data_width
+    tree_constructor = tree_constructor or wrapper.new_constructor(k, sq.codec.ctx)
+    rr = [bytes(r) for r in row_roots]
+    cr = [bytes(c) for c in col_roots]
+    want = {ROW: rr, COL: cr}
+
+    def vec(axis, i):
+        return sq.row(i) if axis == ROW else sq.col(i)
+
+    def complete(axis, i, skip=-1):
+        return all(s is not None for j, s in enumerate(vec(axis, i)) if j != skip)
+
+    def root_ok(axis, i, cells):
+        try:
+            return _axis_root(sq, tree_constructor, axis, i, cells) == want[axis][i]
+        except Exception:  # a tree that cannot be built (push order) does not match its root
+            return False
+
+    def sanity(i):
+        rowc, colc = complete(ROW, i), complete(COL, i)
+        for step, axis in enumerate((ROW, COL, ROW, COL)):
+            if not (rowc if axis == ROW else colc):
+                continue
+            v = vec(axis, i)
+            ok = root_ok(axis, i, v) if step < 2 else \
+                b"".join(sq.codec.encode(v[:k])) == b"".join(v[k:])
+            if not ok:
+                return i * 4 + step
+        return None
+
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        bad = [b for b in ex.map(sanity, range(w)) if b is not None]
+    if bad:
+        b = min(bad)
+        raise ErrByzantineData(ROW if b % 2 == 0 else COL, b // 4)
+
+    def solve(axis, i):  # -> (solved, progress)
+        if complete(axis, i):
+            return True, False
+        shares = vec(axis, i)
+        try:
+            rebuilt = sq.codec.decode(shares)
+        except N.CdaError as e:
+            if e.code == N.E_TOO_FEW:
+                return False, False
+            raise
+        if not root_ok(axis, i, rebuilt):
+            raise ErrByzantineData(axis, i, shares)
+        other = COL if axis == ROW else ROW
+        for j in range(w):
+            cell = (i, j) if axis == ROW else (j, i)
+            if sq.get_cell(*cell) is not None or not complete(other, j, skip=i):
+                continue
+            ov = vec(other, j)
+            ov[i] = rebuilt[j]
+            if not root_ok(other, j, ov):
+                raise ErrByzantineData(other, j, vec(other, j))
+        for j in range(w):
+            cell = (i, j) if axis == ROW else (j, i)
+            if sq.get_cell(*cell) is None:
+                sq.set_cell(*cell, rebuilt[j])
+        return True, True
+
+    while True:
+        solved, progress = True, False
+        for i in range(w):
+            for axis in (ROW, COL):
+                s, p = solve(axis, i)
+                solved, progress = solved and s, progress or p
+        if solved:
+            break
+        if not progress:
+            raise ErrUnrepairableDataSquare()
+    sq._row_roots = np.stack([np.frombuffer(r, np.uint8) for r in rr])
+    sq._col_roots = np.stack([np.frombuffer(c, np.uint8) for c in cr])
 
 
 def _roots_through(sq, tree_constructor):

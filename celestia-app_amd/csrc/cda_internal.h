@@ -10,6 +10,19 @@
 #define CDA_REC_WORDS 24 /* 96-byte node record: 90-byte NMT node + 6 zero bytes */
 #define CDA_REC_BYTES 96
 
+// Test / diagnostic builds (-DCDA_TEST_HOOKS=1: `make hooks` -> cda/libcda_hooks.so) read the A/B switches of the
+// measured experiments from the environment at cda_init / first use.  A release library contains none of
+// their names and reads none of them: its only environment inputs are the deployment options
+// CDA_NUMA_BIND and CDA_COPY_THREADS (cda_build_info() names them).
+#ifndef CDA_TEST_HOOKS
+#define CDA_TEST_HOOKS 0
+#endif
+#if CDA_TEST_HOOKS
+#define CDA_AB_ENV(name) getenv(name)
+#else
+#define CDA_AB_ENV(name) ((const char*)nullptr)
+#endif
+
 namespace cda {
 
 // Leopard field tables (product-side; built in leopard_tables.cpp).
@@ -78,6 +91,13 @@ int launch_trees_lds(const void* d_leaves, void* d_roots, void* d_dah, unsigned*
 int launch_axis_leaf(const uint8_t* d_leaves, int n, uint64_t square_size, uint64_t axis_index, void* d_nodes,
                      unsigned long long* d_status, hipStream_t s);
 int launch_level_generic(const void* d_in, void* d_out, int n_in, hipStream_t s);
+// Roots of ntrees independent wrapper trees of n leaves each (per-axis seam, axisq.cpp): tree t's leaves at
+// d_leaves + t * tree_stride, its axis index d_axis_idx[t]; 96-B root records and status words (first bad leaf or ~0).
+// One workgroup per tree with the tree in LDS: n <= kAxisRootsMaxLeaves (-2 otherwise).
+constexpr int kAxisRootsMaxLeaves = 1024;
+int launch_axis_roots(const uint8_t* d_leaves, long long tree_stride, int n, uint64_t square_size,
+                      const unsigned long long* d_axis_idx, int ntrees, void* d_roots, unsigned long long* d_status,
+                      hipStream_t s);
 // roots of ntrees EDS axes (code_t = d_axes ? d_axes[t] : axis0 + t, code = axis << 24 | index) over
 // leaves [leaf_off, leaf_off + nleaves) (nleaves a power of two, leaf_off a multiple of it), 96-B
 // records into d_roots; d_nodes / d_scratch hold ntrees * nleaves records each.  -2: bad range.

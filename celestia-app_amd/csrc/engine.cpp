@@ -210,7 +210,7 @@ int enqueue_rs(cda_ctx* c, uint32_t k, uint32_t nblocks, const uint8_t* d_ods, u
 // NMT levels + DAH of nblocks blocks whose leaf records are at record offset rec_off.
 // small batches (latency: the consensus path extends one block): all trees + the DAH in one LDS-resident launch
 static bool lds_trees_path(uint32_t k, uint32_t nblocks) {
-  static const int lds_trees = getenv("CDA_TREES_LDS") ? atoi(getenv("CDA_TREES_LDS")) : kLdsTreesMax;  // once
+  static const int lds_trees = CDA_AB_ENV("CDA_TREES_LDS") ? atoi(CDA_AB_ENV("CDA_TREES_LDS")) : kLdsTreesMax;  // once
   return (size_t)nblocks * 4 * k <= (size_t)lds_trees && 2 * k <= 256;
 }
 
@@ -328,18 +328,19 @@ int cda_init(int device, cda_ctx** out) {
     fprintf(stderr, "cda_init: %s initialisation failed: %s\n", fail, hipGetErrorString(hipGetLastError()));
     return CDA_E_DEVICE;
   }
-  if (const char* e = getenv("CDA_REPAIR_OVERLAP")) c->repair_overlap = atoi(e) != 0;
-  if (const char* e = getenv("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
-  if (const char* e = getenv("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
-  if (const char* e = getenv("CDA_STAGING")) c->staging = atoi(e) & 3;
-  if (const char* e = getenv("CDA_CONSENSUS")) c->consensus = atoi(e) != 0;
-  // the one-block path's A/B forms and the huge-page opt-in: read here once, never per call (ctx.h)
-  if (const char* e = getenv("CDA_CONS_IN")) c->cons_in = std::max(0, std::min(2, atoi(e)));
-  if (const char* e = getenv("CDA_CONS_OUT")) c->cons_out = atoi(e) == 2 ? 2 : 0;
-  if (const char* e = getenv("CDA_CONS_STG")) c->cons_stg_mib = std::max(0, atoi(e));
+  if (const char* e = CDA_AB_ENV("CDA_REPAIR_OVERLAP")) c->repair_overlap = atoi(e) != 0;
+  if (const char* e = CDA_AB_ENV("CDA_REPAIR_FUSED")) c->repair_fused_verify = atoi(e) != 0;
+  if (const char* e = CDA_AB_ENV("CDA_REPAIR_EARLY")) c->repair_early = atoi(e) != 0;
+  if (const char* e = CDA_AB_ENV("CDA_STAGING")) c->staging = atoi(e) & 3;
+  if (const char* e = CDA_AB_ENV("CDA_CONSENSUS")) c->consensus = atoi(e) != 0;
+  // the one-block path's A/B forms and the huge-page opt-in (test builds only, CDA_AB_ENV): read here once, never per
+  // call (ctx.h); CDA_COPY_THREADS is a deployment option of every build
+  if (const char* e = CDA_AB_ENV("CDA_CONS_IN")) c->cons_in = std::max(0, std::min(2, atoi(e)));
+  if (const char* e = CDA_AB_ENV("CDA_CONS_OUT")) c->cons_out = atoi(e) == 2 ? 2 : 0;
+  if (const char* e = CDA_AB_ENV("CDA_CONS_STG")) c->cons_stg_mib = std::max(0, atoi(e));
   if (const char* e = getenv("CDA_COPY_THREADS")) c->copy_threads = std::max(1, std::min(64, atoi(e)));
-  if (const char* e = getenv("CDA_HUGE_PAGES")) c->huge_pages = atoi(e) != 0;
-  c->cons_trace = getenv("CDA_CONS_TRACE") != nullptr;
+  if (const char* e = CDA_AB_ENV("CDA_HUGE_PAGES")) c->huge_pages = atoi(e) != 0;
+  c->cons_trace = CDA_AB_ENV("CDA_CONS_TRACE") != nullptr;
   find_local_cpus(c);
   // the streams that overlap each other, created right after `stream` so that they land on distinct hardware
   // queues (HIP assigns streams to its GPU_MAX_HW_QUEUES = 4 queues round-robin)
@@ -374,6 +375,8 @@ void cda_free(cda_ctx* c) {
     for (int i = 0; i < cda_ctx::kJoin; i++)
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     free_consensus(c);  // joins its copy threads first
+    free_axisq(c);
+    if (c->ax.p) (void)hipFree(c->ax.p);
     free_pipeline(c);
     free_staging(c);
     if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
@@ -414,9 +417,10 @@ const char* cda_last_device_error(cda_ctx* c) { return c ? c->last_err.c_str() :
 const char* cda_build_info(void) {
   static const std::string info = [] {
     std::string d;
-    for (const char* t : {rs8_diag_tag(), rs16_diag_tag(), CDA_TEST_HOOKS ? "test_hooks" : ""})
+    for (const char* t : {rs8_diag_tag(), rs16_diag_tag(), axis_diag_tag(), CDA_TEST_HOOKS ? "test_hooks" : ""})
       if (*t) d += (d.empty() ? "" : ",") + std::string(t);
-    return d.empty() ? std::string("release gfx950") : "diagnostic gfx950 " + d;
+    // a release library reads only the deployment options named here (cda_internal.h CDA_AB_ENV)
+    return d.empty() ? std::string("release gfx950; env: CDA_NUMA_BIND, CDA_COPY_THREADS") : "diagnostic gfx950 " + d;
   }();
   return info.c_str();
 }
@@ -438,74 +442,7 @@ int cda_rs_validate_chunk_size(int64_t chunk_size) {
   return (chunk_size > 0 && chunk_size % 64 == 0) ? CDA_OK : CDA_E_SHARD_SIZE;
 }
 
-int cda_rs_encode(cda_ctx* c, uint32_t k, uint32_t shard_len, const uint8_t* data, uint8_t* parity) {
-  CDA_API_TRY
-  if (!c || !data || !parity || k == 0 || k > 32768) return CDA_E_ARG;
-  if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
-  Lock l(c);
-  const size_t bytes = (size_t)k * shard_len;
-  if (int rc = ensure(c, c->ods, bytes)) return rc;
-  if (int rc = ensure(c, c->eds, bytes)) return rc;
-  if (!dev_ok(c, hipMemcpyAsync(c->ods.p, data, bytes, hipMemcpyHostToDevice, c->stream), "H2D")) return CDA_E_DEVICE;
-  RsJob j{};
-  j.src = (const uint8_t*)c->ods.p;
-  j.src_sh = shard_len;
-  j.dst = (uint8_t*)c->eds.p;
-  j.dst_sh = shard_len;
-  j.k = (int)k;
-  j.cw_per_blk = 1;
-  j.nblk = 1;
-  j.shard_len = (int)shard_len;
-  int lr;
-  {
-    ProfScope ps(c, 2 * k <= 256 ? "rs_encode8" : "rs_encode16", c->stream);
-    lr = 2 * k <= 256 ? launch_rs_encode8(j, c->stream) : launch_rs_encode16(j, c->stream);
-  }
-  if (lr == -2) return CDA_E_UNSUPPORTED;
-  if (lr) return CDA_E_DEVICE;
-  if (!dev_ok(c, hipMemcpyAsync(parity, c->eds.p, bytes, hipMemcpyDeviceToHost, c->stream), "D2H")) return CDA_E_DEVICE;
-  if (!dev_ok(c, hipStreamSynchronize(c->stream), "sync")) return CDA_E_DEVICE;
-  flush_profile(c);
-  return CDA_OK;
-  CDA_API_CATCH(c)
-}
-
-int cda_rs_decode(cda_ctx* c, uint32_t k, uint32_t shard_len, uint8_t* shards, const uint8_t* present) {
-  CDA_API_TRY
-  if (!c || !shards || !present || k == 0 || k > 32768) return CDA_E_ARG;
-  if (cda_rs_validate_chunk_size(shard_len)) return CDA_E_SHARD_SIZE;
-  uint32_t np = 0;
-  for (uint32_t i = 0; i < 2 * k; i++) np += present[i] ? 1 : 0;
-  if (np < k) return CDA_E_TOO_FEW;
-  if (np == 2 * k) return CDA_OK;
-  Lock l(c);
-  const size_t bytes = (size_t)2 * k * shard_len;
-  int rc;
-  if ((rc = ensure(c, c->eds, bytes)) || (rc = ensure(c, c->ods, 64 + 2 * (size_t)k))) return rc;
-  // descriptor block: off[1], stride[1], present[2k]
-  std::vector<uint8_t> desc(16 + 2 * (size_t)k);
-  const long long off = 0, stride = shard_len;
-  memcpy(desc.data(), &off, 8);
-  memcpy(desc.data() + 8, &stride, 8);
-  for (uint32_t i = 0; i < 2 * k; i++) desc[16 + i] = present[i] ? 1 : 0;
-  hipStream_t s = c->stream;
-  if (!dev_ok(c, hipMemcpyAsync(c->eds.p, shards, bytes, hipMemcpyHostToDevice, s), "H2D") ||
-      !dev_ok(c, hipMemcpyAsync(c->ods.p, desc.data(), desc.size(), hipMemcpyHostToDevice, s), "H2D"))
-    return CDA_E_DEVICE;
-  {
-    ProfScope ps(c, "rs_decode", s);
-    const uint8_t* d = (const uint8_t*)c->ods.p;
-    const int lr = launch_rs_decode((uint8_t*)c->eds.p, (const long long*)d, (const long long*)(d + 8), d + 16, 1,
-                                    (int)k, (int)shard_len, s);
-    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
-  }
-  if (!dev_ok(c, hipMemcpyAsync(shards, c->eds.p, bytes, hipMemcpyDeviceToHost, s), "D2H") ||
-      !dev_ok(c, hipStreamSynchronize(s), "sync"))
-    return CDA_E_DEVICE;
-  flush_profile(c);
-  return CDA_OK;
-  CDA_API_CATCH(c)
-}
+// cda_rs_encode, cda_rs_decode, cda_nmt_axis_root: the per-axis seams, axisq.cpp
 
 int cda_extend_commit_device(cda_ctx* c, uint32_t k, uint32_t nblocks, const void* d_ods, void* d_eds, void* d_roots,
                              void* d_dah, void* d_status, void* stream) {
@@ -783,69 +720,6 @@ int cda_dah_hash(cda_ctx* c, uint32_t n, const uint8_t* row_roots, const uint8_t
       !dev_ok(c, hipStreamSynchronize(s), "sync"))
     return CDA_E_DEVICE;
   flush_profile(c);
-  return CDA_OK;
-  CDA_API_CATCH(c)
-}
-
-int cda_nmt_axis_root(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uint32_t n, uint32_t leaf_len,
-                      const uint8_t* leaves, uint8_t* root, cda_err_info* err) {
-  CDA_API_TRY
-  set_err(err, CDA_OK, -1, -1, -1, -1);
-  if (!c || !root || (n && !leaves) || square_size == 0) return CDA_E_ARG;
-  // ErasuredNamespacedMerkleTree.Push checks (nmt_wrapper.go:94-99) happen leaf by leaf in the
-  // reference, before nmt's order check of the same leaf: the bounds check fails first at leaf 0
-  // (axis index out of range) or at leaf 2k (pushed past the square), the namespace-length check at
-  // leaf 0.  An order violation at a leaf j < 2k therefore wins over a push past the square; the
-  // device pass below only looks at the leaves the reference would have accepted.
-  if (n > 0 && axis_index + 1 > 2 * square_size)
-    return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, 0, -1), CDA_E_PUSH_PAST;
-  if (n > 0 && leaf_len < CDA_NAMESPACE_SIZE)
-    return set_err(err, CDA_E_NS_SHORT, -1, (int)axis_index, 0, -1), CDA_E_NS_SHORT;
-  const uint64_t push_limit = 2 * square_size;
-  const bool past = (uint64_t)n > push_limit;
-  if (past) n = (uint32_t)push_limit;
-  if (n == 0) {  // EmptyRoot: 0x00*58 ‖ SHA256("")
-    static const uint8_t kEmpty[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
-                                       0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
-                                       0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
-    memset(root, 0, 58);
-    memcpy(root + 58, kEmpty, 32);
-    return CDA_OK;
-  }
-  if (leaf_len != CDA_SHARE) return CDA_E_UNSUPPORTED;
-  Lock l(c);
-  const size_t in_b = (size_t)n * leaf_len, rec_b = (size_t)n * CDA_REC_BYTES;
-  int rc;
-  if ((rc = ensure(c, c->ods, in_b)) || (rc = ensure(c, c->leaf, rec_b)) || (rc = ensure(c, c->scratch, rec_b)) ||
-      (rc = ensure(c, c->status, 8)))
-    return rc;
-  hipStream_t s = c->stream;
-  if (!dev_ok(c, hipMemcpyAsync(c->ods.p, leaves, in_b, hipMemcpyHostToDevice, s), "H2D") ||
-      !dev_ok(c, hipMemsetAsync(c->status.p, 0xFF, 8, s), "memset"))
-    return CDA_E_DEVICE;
-  {
-    ProfScope ps(c, "axis_leaf", s);
-    if (launch_axis_leaf((const uint8_t*)c->ods.p, (int)n, square_size, axis_index, c->leaf.p,
-                         (unsigned long long*)c->status.p, s))
-      return CDA_E_DEVICE;
-  }
-  void* bufs[2] = {c->leaf.p, c->scratch.p};
-  int cur = 0;
-  for (uint32_t cnt = n; cnt > 1; cnt = (cnt + 1) / 2) {
-    ProfScope ps(c, "nmt_level_generic", s);
-    if (launch_level_generic(bufs[cur], bufs[cur ^ 1], (int)cnt, s)) return CDA_E_DEVICE;
-    cur ^= 1;
-  }
-  uint8_t rec[CDA_REC_BYTES];
-  uint64_t st = 0;
-  if (!dev_ok(c, hipMemcpyAsync(rec, bufs[cur], CDA_REC_BYTES, hipMemcpyDeviceToHost, s), "D2H") ||
-      !dev_ok(c, hipMemcpyAsync(&st, c->status.p, 8, hipMemcpyDeviceToHost, s), "D2H") ||
-      !dev_ok(c, hipStreamSynchronize(s), "sync"))
-    return CDA_E_DEVICE;
-  flush_profile(c);
-  if (st != ~0ull) return set_err(err, CDA_E_NS_ORDER, -1, (int)axis_index, (int)st, -1), CDA_E_NS_ORDER;
-  if (past) return set_err(err, CDA_E_PUSH_PAST, -1, (int)axis_index, (int)push_limit, -1), CDA_E_PUSH_PAST;
-  memcpy(root, rec, CDA_NODE_SIZE);
   return CDA_OK;
   CDA_API_CATCH(c)
 }

@@ -126,12 +126,17 @@ __global__ void __launch_bounds__(256) nmt_levels_kernel(LevelSet ls, int log2w,
   const unsigned tree = col ? (r2 & (w - 1)) : (r2 >> log2n_out);
   const unsigned j = col ? (r2 >> log2w) : (r2 & ((1u << log2n_out) - 1));
   __shared__ uint4 s_ns[256 * 8];  // per thread: the first 64 B of both children of the node being hashed
+#if CDA_NS_NOSWZ  // diagnostic A/B: the round-5 layout (every lane's piece i in the same banks)
+  const int ns_x = 0;
+#else
+  const int ns_x = (int)((threadIdx.x ^ (threadIdx.x >> 3)) & 7);  // piece swizzle: conflict-free LDS (nmt_dev.h)
+#endif
   for (int q = 1; q <= M; q++) {
     const unsigned cnt = 1u << (M - q);  // nodes of this subtree at level l_in + q
     for (unsigned t = 0; t < cnt; t++) {
       const unsigned i = j * cnt + t;
       hash_node_mem(level_rec(ls.lv[q - 1], b, col, tree, 2 * i), level_rec(ls.lv[q - 1], b, col, tree, 2 * i + 1),
-                    level_rec(ls.lv[q], b, col, tree, i), true, s_ns + threadIdx.x * 8);
+                    level_rec(ls.lv[q], b, col, tree, i), true, s_ns + threadIdx.x * 8, ns_x);
     }
     // the next level reads what this thread just stored
     if (q < M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -853,6 +858,74 @@ int launch_axes_verify(const uint8_t* d_eds, int k, const int* d_axes, int ntree
     return -1;
   hipLaunchKernelGGL(axes_verify_kernel, dim3(ntrees), dim3(256), lds, s, d_eds, k, log2w, d_axes, d_want_rows,
                      d_want_cols, d_flag, base, per_tree ? 1 : 0);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Roots of independent wrapper trees handed over through the per-axis seam (ErasuredNamespacedMerkleTree Push x n +
+// Root, pkg/wrapper/nmt_wrapper.go:93-124; axisq.cpp coalesces concurrent calls into one launch).  Tree t's n leaves
+// are contiguous 512-B shares at leaves + t * tree_stride; its axis index axis_idx[t] and the square size give the
+// quadrant rule (leaf i hashes its own namespace iff i < square_size and axis index < square_size, else 0xFF x 29,
+// :138-140).  One workgroup per tree: leaf records in LDS, levels folded in place (level l node i at slot i << l; a
+// last odd node keeps its slot, which is the nmt split at the largest power of two below n), the root record to
+// roots[t] and the first leaf whose Push order check fails (nmt ErrInvalidPushOrder) to status[t] (~0 when none).
+// Replaces the leaf launch + ceil(log2 n) level launches of the generic single-tree path.
+__global__ void __launch_bounds__(256) axis_roots_kernel(const uint8_t* __restrict__ leaves, long long tree_stride,
+                                                         int n, unsigned long long square_size,
+                                                         const unsigned long long* __restrict__ axis_idx,
+                                                         uint4* __restrict__ roots,
+                                                         unsigned long long* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lnodes[];  // [n][6]
+  __shared__ unsigned bad;
+  const int t = blockIdx.x;
+  const unsigned long long axis = axis_idx[t];
+  const uint8_t* base = leaves + (size_t)t * tree_stride;
+  if (threadIdx.x == 0) bad = 0xFFFFFFFFu;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const bool q0 = (unsigned long long)i < square_size && axis < square_size;
+    const uint4* sh = reinterpret_cast<const uint4*>(base + (size_t)i * CDA_SHARE);
+    uint32_t A[16];
+    load16(sh, A);
+    if (q0 && (unsigned long long)(i + 1) < square_size && i + 1 < n) {
+      const uint4* p = sh + CDA_SHARE / 16;
+      const uint4 v0 = p[0], v1 = p[1];
+      uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (ns_cmp(nb, A) < 0) atomicMin(&bad, (unsigned)(i + 1));
+    }
+    leaf_record<false>(sh, A, q0, lnodes + (size_t)i * 6);
+  }
+  __syncthreads();
+  int l = 0;
+  for (int c = n; c > 1; c = (c + 1) >> 1) {
+    l++;
+    const int pairs = c >> 1;
+    if (pairs >= 64) {
+      for (int i = threadIdx.x; i < pairs; i += blockDim.x)
+        hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
+                      lnodes + ((size_t)i << l) * 6);
+    } else if (threadIdx.x < 64) {  // a small level: the whole wave computes (lanes past the last pair store nothing)
+      const int i = (int)threadIdx.x < pairs ? (int)threadIdx.x : 0;
+      hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
+                    lnodes + ((size_t)i << l) * 6, (int)threadIdx.x < pairs);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) roots[(size_t)t * 6 + threadIdx.x] = lnodes[threadIdx.x];
+  if (threadIdx.x == 0) status[t] = bad == 0xFFFFFFFFu ? ~0ull : (unsigned long long)bad;
+}
+
+int launch_axis_roots(const uint8_t* d_leaves, long long tree_stride, int n, uint64_t square_size,
+                      const unsigned long long* d_axis_idx, int ntrees, void* d_roots, unsigned long long* d_status,
+                      hipStream_t s) {
+  if (ntrees <= 0) return 0;
+  if (n < 1 || n > kAxisRootsMaxLeaves) return -2;
+  const size_t lds = (size_t)n * CDA_REC_BYTES;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)axis_roots_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(axis_roots_kernel, dim3(ntrees), dim3(256), lds, s, d_leaves, tree_stride, n,
+                     (unsigned long long)square_size, d_axis_idx, (uint4*)d_roots, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -54,7 +54,7 @@ struct RepairTrace {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
   std::string line;
   RepairTrace() {
-    static const bool env = getenv("CDA_REPAIR_TRACE") && atoi(getenv("CDA_REPAIR_TRACE")) != 0;
+    static const bool env = CDA_AB_ENV("CDA_REPAIR_TRACE") && atoi(CDA_AB_ENV("CDA_REPAIR_TRACE")) != 0;
     on = env;
   }
   void mark(const char* what) {

@@ -611,7 +611,7 @@ int launch_rs_encode8(const RsJob& j, hipStream_t s) {
   // workgroups of U units (32 B each) instead, so the pass spreads over the chip.  CDA_RS8_LAT_U picks U
   // (0 = off; default 4); results are identical either way (both encoders are bit-exact).
   static const int lat_u = [] {
-    const char* e = getenv("CDA_RS8_LAT_U");
+    const char* e = CDA_AB_ENV("CDA_RS8_LAT_U");
     const int v = e ? atoi(e) : 4;
     return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
   }();
@@ -900,7 +900,7 @@ int launch_rs_encode16(const RsJob& j, hipStream_t s) {
   // k = 512 codewords of whole 512-B shards: the register-resident encoder (rs16_kernels.hip); CDA_RS16=lds forces
   // this LDS encoder (same bytes) for A/B runs
   static const bool force_lds = [] {
-    const char* e = getenv("CDA_RS16");
+    const char* e = CDA_AB_ENV("CDA_RS16");
     return e && e[0] == 'l';
   }();
   if (!force_lds && rs16_reg_eligible(j)) return launch_rs_encode16_reg(j, g_cpoly16[dev], s);
@@ -928,7 +928,7 @@ int launch_rs_encode16(const RsJob& j, hipStream_t s) {
   // 32 KiB (U = 1, 5 workgroups per CU) rows 0.47 + cols 0.83 ms per 2 squares, 64 KiB (U = 2) 0.56 + 1.03,
   // 128 KiB 0.83 + 1.55 -- occupancy wins over the extra lane-masked layers.
   static const size_t budget = [] {
-    const char* e = getenv("CDA_RS16_LDS_KB");
+    const char* e = CDA_AB_ENV("CDA_RS16_LDS_KB");
     return (size_t)(e ? atoi(e) : 32) * 1024;
   }();
   int U = 8;

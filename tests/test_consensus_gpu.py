@@ -3,7 +3,9 @@ as PrepareProposal / ProcessProposal call da.ExtendShares (app/prepare_proposal.
 app/process_proposal.go:137-151).  The input goes up in row bands (or one copy for roots only), Q0 is copied host to
 host by a copy pool, Q1 and the bottom half come back while the device hashes, and the output form follows the
 caller's buffer (pinned / written before / fresh and untouched).  Every case is bit-exact against the oracle, and
-against the serial form (a context opened with CDA_CONSENSUS=0) for the error reports."""
+against the serial form (a context opened with CDA_CONSENSUS=0) for the error reports.  The A/B switches exist only
+in the test-hooks build (cda/libcda_hooks.so, same sources), so the forms below open their contexts on it; the release
+library always takes the default form (test_one_block_fresh_buffers, test_one_block_registered_caller_buffers)."""
 import threading
 
 import numpy as np
@@ -19,10 +21,11 @@ def serial_ctx():
     import os
 
     import cda
+    from cda import _native as N
     old = os.environ.get("CDA_CONSENSUS")
     os.environ["CDA_CONSENSUS"] = "0"
     try:
-        c = cda.Context(0)
+        c = cda.Context(0, lib_path=N.HOOKS_LIB_PATH)
     finally:
         if old is None:
             del os.environ["CDA_CONSENSUS"]
@@ -60,13 +63,14 @@ def test_one_block_forms(monkeypatch, cons_in, cons_out, stg, huge):
     pinned slab, 0 = all pageable, 3 MiB) and the opt-in huge-page hint (CDA_HUGE_PAGES), fresh and written output
     buffers, k = 16 and 128.  The knobs are read once at cda_init, so each form gets its own context."""
     import cda
+    from cda import _native as N
     monkeypatch.setenv("CDA_CONS_IN", cons_in)
     monkeypatch.setenv("CDA_CONS_OUT", cons_out)
     if stg is not None:
         monkeypatch.setenv("CDA_CONS_STG", stg)
     if huge is not None:
         monkeypatch.setenv("CDA_HUGE_PAGES", huge)
-    c = cda.Context(0)
+    c = cda.Context(0, lib_path=N.HOOKS_LIB_PATH)
     try:
         for k in (16, 128):
             ods = O.gen_ods(k, 0xF0F0 + k)

@@ -58,7 +58,7 @@ def test_release_library_is_bit_exact_with_fault_injection_set(monkeypatch):
     returns bit-exact results: no environment variable can make a release build fail."""
     import cda
     from cda import _native as N
-    assert N.build_info() == "release gfx950"
+    assert N.build_info().startswith("release gfx950")
     for site in ("alloc", "thread", "entry"):
         monkeypatch.setenv("CDA_FAULT_INJECT", site)
         c = cda.Context(0)  # fresh: every workspace buffer and helper thread is created under the variable
