@@ -270,8 +270,12 @@ int cda_host_unregister(cda_ctx* c, void* p) {
   CDA_API_TRY
   if (!c || !p) return CDA_E_ARG;
   Lock l(c);
-  // every DMA this context enqueued into or out of the range has finished before the pages are released
-  if (!dev_ok(c, hipStreamSynchronize(c->stream), "sync")) return CDA_E_DEVICE;
+  // Every DMA this context enqueued into or out of the range has finished before the pages are released: the
+  // synchronous entry points return only after their copies completed, and the copy streams (h2d / d2h: the batch
+  // pipeline, the one-block path, repair; aux: repair's verification) and the main stream are drained here as well,
+  // so this holds whatever a future entry point leaves in flight.
+  for (hipStream_t s : {c->stream, c->h2d_stream, c->d2h_stream, c->aux_stream})
+    if (s && !dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
   return dev_ok(c, hipHostUnregister(p), "hipHostUnregister") ? CDA_OK : CDA_E_DEVICE;
   CDA_API_CATCH(c)
 }

@@ -483,8 +483,13 @@ int split_impl(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const
 // A failure on any device of the handle (an RCCL group call is issued per device; ncclCommInitAll reports into
 // device 0) is surfaced through cda_last_device_error(cda_multi_context(m, 0)): every device's message, each named
 // by its handle index and HIP device, with the RCCL error string.
+// Every context's lock is held from the clearing of last_err to the combined message (a concurrent call on
+// a handle from cda_multi_context writes the same string under that lock); split_impl takes the handle's split mutex
+// and re-enters these (recursive) locks.
 int split_call(cda_multi* m, uint32_t k, const uint8_t* h_ods, const void* const* d_slabs, uint8_t* eds,
                uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, cda_err_info* err) {
+  std::vector<std::unique_ptr<Lock>> locks;
+  for (auto* c : m->ctx) locks.emplace_back(new Lock(c));
   for (auto* c : m->ctx) c->last_err.clear();
   const int rc = split_impl(m, k, h_ods, d_slabs, eds, row_roots, col_roots, dah, err);
   if (rc == CDA_E_DEVICE || rc == CDA_E_NOMEM || rc == CDA_E_INTERNAL) {

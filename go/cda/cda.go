@@ -86,7 +86,8 @@ func toErr(rc C.int, info *C.cda_err_info) error {
 // Context is one cda_ctx (one GPU).  Its calls are serialised by libcda, so one Context may be shared by the
 // goroutines rsmt2d fans out per axis.
 type Context struct {
-	c *C.cda_ctx
+	c      *C.cda_ctx
+	closed bool // set by Close under the pools' locks: slabs of a closed context are never pooled again
 }
 
 // NewContext binds HIP device `device`.
@@ -98,12 +99,21 @@ func NewContext(device int) (*Context, error) {
 	return &Context{c: c}, nil
 }
 
-// Close releases the context.
+// Close releases the context: its free pooled slabs are unregistered and dropped, the slabs squares still hold are
+// unregistered (they stay valid Go memory and are dropped when they come back), then the context is freed.
 func (x *Context) Close() {
-	if x.c != nil {
-		C.cda_free(x.c)
-		x.c = nil
+	if x.c == nil {
+		return
 	}
+	edsPool.mu.Lock()
+	sharePool.mu.Lock()
+	x.closed = true
+	sharePool.mu.Unlock()
+	edsPool.mu.Unlock()
+	x.Trim()
+	x.unregisterInUse()
+	C.cda_free(x.c)
+	x.c = nil
 }
 
 var (

@@ -13,6 +13,8 @@ import (
 	"runtime"
 	"sort"
 	"testing"
+	"time"
+	"unsafe"
 
 	"github.com/celestiaorg/go-square/blob"
 	"github.com/celestiaorg/go-square/inclusion"
@@ -162,9 +164,24 @@ func TestDataAvailabilityHeaderFromSharesMatchesCPUPath(t *testing.T) {
 	require.Error(t, err)
 }
 
+// waitForFree runs garbage collections until a freed slab is back in the pool (finalizers run asynchronously after
+// the cycle that finds the slab unreachable), at most ~2 s.
+func waitForFree(t *testing.T, recycledBefore uint64) {
+	for i := 0; i < 200; i++ {
+		runtime.GC()
+		runtime.Gosched()
+		if cda.Stats().Recycled > recycledBefore {
+			return
+		}
+		time.Sleep(10 * time.Millisecond)
+	}
+	t.Fatalf("no slab came back through the finalizer")
+}
+
 // TestEDSPoolRecycles: ExtendShares' squares live in pooled page-locked slabs; after the squares (and every slice of
 // their cells) are unreachable, a garbage collection returns the slabs, later squares reuse them, and every square
-// stays bit-exact however its slab came to it.
+// stays bit-exact however its slab came to it.  Slabs are tracked by address only (uintptr): a map of *byte would
+// itself keep every slab reachable (ADVICE r05).
 func TestEDSPoolRecycles(t *testing.T) {
 	r := rand.New(rand.NewSource(7))
 	k := 64 // 8 MiB EDS: pooled
@@ -172,18 +189,19 @@ func TestEDSPoolRecycles(t *testing.T) {
 	ref, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
 	require.NoError(t, err)
 	want := ref.Flattened()
-	seen := map[*byte]int{}
+	seen := map[uintptr]int{}
 	for i := 0; i < 12; i++ {
+		before := cda.Stats().Recycled
 		eds, err := cda.ExtendShares(s)
 		require.NoError(t, err)
 		flat := eds.Flattened()
 		require.Equal(t, want, flat, "call %d", i)
-		seen[&flat[0][0]]++
+		seen[uintptr(unsafe.Pointer(&flat[0][0]))]++
 		eds, flat = nil, nil
-		runtime.GC()
-		runtime.GC() // the finalizer of the slab runs after the first cycle finds it unreachable
+		waitForFree(t, before)
 	}
 	require.Less(t, len(seen), 12, "no slab was reused")
+	require.Greater(t, cda.Stats().Hits, uint64(0))
 	// a square whose cells are still referenced keeps its slab: the next squares get other slabs
 	keep, err := cda.ExtendShares(s)
 	require.NoError(t, err)
@@ -199,6 +217,80 @@ func TestEDSPoolRecycles(t *testing.T) {
 	}
 	require.Equal(t, cell, row0)
 	require.Equal(t, want[0], row0)
+}
+
+// TestReleaseReturnsSlabAtOnce: Release hands a square's slab back without a garbage collection; the next square
+// reuses it (same address, a pool hit) and is bit-exact; a square not on a pooled slab is ignored.
+func TestReleaseReturnsSlabAtOnce(t *testing.T) {
+	r := rand.New(rand.NewSource(8))
+	k := 64
+	s := sortedShares(r, k*k)
+	a, err := cda.ExtendShares(s)
+	require.NoError(t, err)
+	want := a.Flattened()
+	wantCopy := make([][]byte, len(want))
+	for i := range want {
+		wantCopy[i] = append([]byte(nil), want[i]...)
+	}
+	base := uintptr(unsafe.Pointer(&want[0][0]))
+	want = nil
+	st := cda.Stats()
+	require.True(t, cda.Release(a))
+	require.Equal(t, st.Released+1, cda.Stats().Released)
+	b, err := cda.ExtendShares(s)
+	require.NoError(t, err)
+	fb := b.Flattened()
+	require.Equal(t, base, uintptr(unsafe.Pointer(&fb[0][0])), "the released slab is reused")
+	require.Equal(t, wantCopy, fb)
+	ref, err := rsmt2d.ComputeExtendedDataSquare(s, rsmt2d.NewLeoRSCodec(), wrapper.NewConstructor(uint64(k)))
+	require.NoError(t, err)
+	require.False(t, cda.Release(ref))
+}
+
+// TestRepairPooledAndInPlace: Repair of an imported square copies into a pooled slab; Repair of a square from
+// ExtendShares whose cells were erased runs in place on its own slab (no copy); both restore the square.
+func TestRepairPooledAndInPlace(t *testing.T) {
+	r := rand.New(rand.NewSource(9))
+	k := 64
+	w := 2 * k
+	s := sortedShares(r, k*k)
+	full, err := cda.ExtendShares(s)
+	require.NoError(t, err)
+	rows, _ := full.RowRoots()
+	cols, _ := full.ColRoots()
+	want := make([][]byte, w*w)
+	for i, c := range full.Flattened() {
+		want[i] = append([]byte(nil), c...)
+	}
+	damaged := func(cells [][]byte) [][]byte {
+		out := make([][]byte, len(cells))
+		for i, c := range cells {
+			if r.Intn(2) == 0 {
+				out[i] = c
+			}
+		}
+		return out
+	}
+	copied := make([][]byte, w*w)
+	for i := range want {
+		copied[i] = append([]byte(nil), want[i]...)
+	}
+	imp := damaged(copied)
+	require.NoError(t, cda.Repair(mustCtx(t), imp, rows, cols))
+	require.Equal(t, want, imp)
+	inPlace := damaged(full.Flattened())
+	base := uintptr(unsafe.Pointer(&full.Flattened()[0][0]))
+	require.NoError(t, cda.Repair(mustCtx(t), inPlace, rows, cols))
+	require.Equal(t, want, inPlace)
+	for i, c := range inPlace {
+		require.Equal(t, base+uintptr(i*cda.ShareSize), uintptr(unsafe.Pointer(&c[0])), "cell %d repaired in place", i)
+	}
+}
+
+func mustCtx(t *testing.T) *cda.Context {
+	x, err := cda.Default()
+	require.NoError(t, err)
+	return x
 }
 
 func TestExtendSquareSplitMatchesCPUPath(t *testing.T) {
