@@ -123,7 +123,10 @@ func importWithRoots(ctx *Context, eds []byte, w, n int, rows, cols []byte) (*rs
 	cache.roots[1] = split(cols, w)
 	cache.used[0] = make([]bool, w)
 	cache.used[1] = make([]bool, w)
-	sq, err := rsmt2d.ImportExtendedDataSquare(split(eds, w*w), NewCodecOn(ctx), cache.constructor(ctx, uint64(w/2)))
+	// The square carries the reference's CPU codec for whatever rsmt2d does with it later axis by axis (Repair after
+	// cells are erased, re-extension): per axis through host buffers the CPU codec is not slower than the GPU's
+	// (DESIGN.md §12.1).  cda.Repair repairs a whole square on the GPU in one call.
+	sq, err := rsmt2d.ImportExtendedDataSquare(split(eds, w*w), rsmt2d.NewLeoRSCodec(), cache.constructor(ctx, uint64(w/2)))
 	if err != nil {
 		return nil, err
 	}

@@ -13,6 +13,8 @@ import (
 	"sync"
 
 	"github.com/celestiaorg/rsmt2d"
+
+	"github.com/celestiaorg/celestia-app/v2/pkg/wrapper"
 )
 
 var parityNamespace = bytes.Repeat([]byte{0xFF}, NamespaceSize) // appns.ParitySharesNamespace
@@ -90,7 +92,8 @@ func (t *Tree) Root() ([]byte, error) {
 // rootCache hands out the roots the GPU computed for a whole square, once per axis: the computeRoots pass that
 // importWithRoots runs on the freshly imported square (before any caller can change a cell) reads them instead of
 // re-hashing (cda_extend_commit already checked every push order).  Every later tree of the square -- rsmt2d builds
-// one only after cells changed, e.g. in Repair -- is a full Tree that hashes what is pushed to it.
+// one only after cells changed, e.g. in Repair -- is the reference's wrapper tree (pkg/wrapper, hashing on the CPU):
+// one axis root through host memory is not faster on the GPU (DESIGN.md §12.1).
 type rootCache struct {
 	mu    sync.Mutex
 	roots [2][][]byte // [rsmt2d.Row / rsmt2d.Col][index]
@@ -141,6 +144,6 @@ func (c *rootCache) constructor(ctx *Context, squareSize uint64) rsmt2d.TreeCons
 		if first {
 			return &cachedTree{root: c.roots[a][idx], squareSize: squareSize, axisIndex: uint64(axisIndex)}
 		}
-		return newTree(ctx, squareSize, uint64(axisIndex))
+		return wrapper.NewConstructor(squareSize)(axis, axisIndex)
 	}
 }

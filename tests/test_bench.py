@@ -46,6 +46,17 @@ def test_bench_spawns_four_ranks():
     assert r["k512_split"]["G"] == 4
 
 
+def test_bench_spawns_eight_ranks():
+    """The driver's N = 8 line: 8 gloo ranks, every rank reports, and config C5's split helper
+    answers for G = 8 with its fields (an error field when it fails, never the exit code)."""
+    r = _run_bench("--gpus", "8", "--dry-run")
+    assert r["n_gpus"] == 8 and r["ranks_seen"] == 8 and r["max_rank"] == 7
+    _check_ranks(r, 8)
+    split = r["k512_split"]
+    assert split.get("G") == 8 or "error" in split
+    assert set(split) <= {"dry_run", "G", "helper_wall_s", "error"}
+
+
 def test_bench_split_helper_failure_is_a_field():
     """A helper that cannot run becomes an error field, not the bench's exit code."""
     sys.path.insert(0, ROOT)

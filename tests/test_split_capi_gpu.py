@@ -53,6 +53,28 @@ def test_split_roots_only_and_device_input():
         m.close()
 
 
+@pytest.mark.parametrize("k,G", [(512, 8), (512, 4), (256, 8)])
+def test_split_device_input_matches_oracle_dah(k, G):
+    """cda_multi_extend_commit_split_device -- each device's ODS row slab already in its HBM, the form a multi-GPU
+    node feeds config C5 with -- at k = 512 over G = 8: every root and the DAH equal the
+    oracle's (the replica transport runs the same plan and kernels as RCCL)."""
+    import torch
+    ods = O.gen_ods(k, 0xC0FFEE)
+    rc, _, rr_o, cr_o, dah_o = O.extend_commit(ods, want_eds=False)
+    assert rc == 0
+    m = _multi(G)
+    try:
+        rows = torch.from_numpy(ods.reshape(k, k, 512)).cuda()
+        rp = k // G
+        slabs = [rows[g * rp:(g + 1) * rp].contiguous() for g in range(G)]
+        torch.cuda.synchronize()
+        for _ in range(2):
+            rr, cr, dah = m.extend_commit_split_device(k, [sl.data_ptr() for sl in slabs])
+            assert dah == dah_o and np.array_equal(rr, rr_o) and np.array_equal(cr, cr_o)
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("G", [1, 2, 4])
 def test_split_push_order_errors_match_block_path(ctx, G):
     """Swapped shares: a row violation, a column violation, a swap that breaks no axis order (row 4's last share
