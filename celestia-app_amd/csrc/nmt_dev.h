@@ -193,12 +193,13 @@ __device__ __forceinline__ void ld4(const uint4* p, uint32_t* w) {  // 4 x 16 B 
 // fenced: 89 VGPRs (5 waves/SIMD) instead of 205 when both children stayed in
 // registers.
 // ns_lds (optional): this thread's 128-B LDS slot; the first 64 B of both children are parked there when loaded for
-// blocks 0 / 1 and the namespace range is read back from it instead of from global memory.  Its eight 16-B pieces are
-// stored at piece index ^ ns_x (ns_x in 0..7): with the slots 128 B apart every lane's piece i would sit in the same
-// banks (8-way conflicts on ds_write_b128 and ds_read_b128); ns_x = (t ^ t >> 3) & 7 of the lane
-// spreads both instructions' lane groups over all banks (nmt_levels_kernel).
+// blocks 0 / 1 and the namespace range is read back from it instead of from global memory.  With the slots 128 B
+// apart, lane i's piece j shares banks with every other lane's piece j (8-way conflicts on ds_write_b128 /
+// ds_read_b128).  Swizzling the pieces (piece ^ ((lane ^ lane >> 3) & 7)) removed every conflict of the levels 1-2
+// launch (SQ_LDS_BANK_CONFLICT 132 M -> 0) but moved blocks/s by +0.3 / +0.9 % on two boxes (the kernel is
+// VALU-bound): below the 1 % bar, not kept.
 __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po, bool store = true,
-                                              uint4* ns_lds = nullptr, int ns_x = 0) {
+                                              uint4* ns_lds = nullptr) {
   uint32_t st[8], m[16];
   sha256_init(st);
   // message = 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits); 48 words
@@ -210,7 +211,7 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
     for (int i = 1; i < 16; i++) m[i] = be_window(L[i - 1], L[i], 3);
     if (ns_lds)
 #pragma unroll
-      for (int i = 0; i < 4; i++) ns_lds[i ^ ns_x] = make_uint4(L[4 * i], L[4 * i + 1], L[4 * i + 2], L[4 * i + 3]);
+      for (int i = 0; i < 4; i++) ns_lds[i] = make_uint4(L[4 * i], L[4 * i + 1], L[4 * i + 2], L[4 * i + 3]);
   }
   sha256_compress_fenced(st, m);
   {  // block 1: words 16..31 <- L words 15..22, R words 0..8
@@ -219,8 +220,7 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
     ld4(launder_after(pr, st[0]), R);      // words 0..15: only 0..11 are read
     if (ns_lds)
 #pragma unroll
-      for (int i = 0; i < 4; i++)
-        ns_lds[(4 + i) ^ ns_x] = make_uint4(R[4 * i], R[4 * i + 1], R[4 * i + 2], R[4 * i + 3]);
+      for (int i = 0; i < 4; i++) ns_lds[4 + i] = make_uint4(R[4 * i], R[4 * i + 1], R[4 * i + 2], R[4 * i + 3]);
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int wi = 16 + i;
@@ -249,12 +249,8 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
   if (ns_lds) {
     uint32_t z = 0;  // an offset tied to the last compression keeps the LDS reads below it (pointer stays in LDS)
     asm volatile("" : "+v"(z) : "v"(st[0]));
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint4 a = ns_lds[z + (i ^ ns_x)], b = ns_lds[z + ((4 + i) ^ ns_x)];
-      L[4 * i] = a.x, L[4 * i + 1] = a.y, L[4 * i + 2] = a.z, L[4 * i + 3] = a.w;
-      R[4 * i] = b.x, R[4 * i + 1] = b.y, R[4 * i + 2] = b.z, R[4 * i + 3] = b.w;
-    }
+    ld4(ns_lds + z, L);
+    ld4(ns_lds + z + 4, R);
 #pragma unroll
     for (int i = 0; i < 16; i++) asm volatile("" : "+v"(L[i]), "+v"(R[i]));  // values, not a select of addresses
   } else {

@@ -126,17 +126,12 @@ __global__ void __launch_bounds__(256) nmt_levels_kernel(LevelSet ls, int log2w,
   const unsigned tree = col ? (r2 & (w - 1)) : (r2 >> log2n_out);
   const unsigned j = col ? (r2 >> log2w) : (r2 & ((1u << log2n_out) - 1));
   __shared__ uint4 s_ns[256 * 8];  // per thread: the first 64 B of both children of the node being hashed
-#if CDA_NS_NOSWZ  // diagnostic A/B: the round-5 layout (every lane's piece i in the same banks)
-  const int ns_x = 0;
-#else
-  const int ns_x = (int)((threadIdx.x ^ (threadIdx.x >> 3)) & 7);  // piece swizzle: conflict-free LDS (nmt_dev.h)
-#endif
   for (int q = 1; q <= M; q++) {
     const unsigned cnt = 1u << (M - q);  // nodes of this subtree at level l_in + q
     for (unsigned t = 0; t < cnt; t++) {
       const unsigned i = j * cnt + t;
       hash_node_mem(level_rec(ls.lv[q - 1], b, col, tree, 2 * i), level_rec(ls.lv[q - 1], b, col, tree, 2 * i + 1),
-                    level_rec(ls.lv[q], b, col, tree, i), true, s_ns + threadIdx.x * 8, ns_x);
+                    level_rec(ls.lv[q], b, col, tree, i), true, s_ns + threadIdx.x * 8);
     }
     // the next level reads what this thread just stored
     if (q < M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
