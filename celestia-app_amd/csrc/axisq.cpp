@@ -286,31 +286,34 @@ void hand_over(AxisQueue* q) {
 // on return.  Every request of the batch is kDone when it returns, and the staging is free again.
 void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* self) {
   q->leader = true;
-  std::vector<AxisReq*> batch;
-  size_t bytes = 0;
-  std::vector<AxisReq*> rest;
-  for (AxisReq* r : q->pending) {
-    if (batch.empty() || bytes + r->bytes() <= kBatchBytes || r == self) {
-      batch.push_back(r);
-      bytes += r->bytes();
-    } else {
-      rest.push_back(r);
-    }
-  }
-  q->pending.swap(rest);
+  std::vector<AxisReq*> batch, rest;
   Layout L;
   int fail = CDA_OK;
-  try {
+  try {  // nothing below changes the queue until it has succeeded (an allocation failure leaves it as it was)
+    batch.reserve(q->pending.size());
+    rest.reserve(q->pending.size());
+    size_t bytes = 0;
+    for (AxisReq* r : q->pending) {
+      if (batch.empty() || bytes + r->bytes() <= kBatchBytes || r == self) {
+        batch.push_back(r);
+        bytes += r->bytes();
+      } else {
+        rest.push_back(r);
+      }
+    }
     plan(batch, L);
     if (!ensure_host(c, q, L.total)) fail = CDA_E_NOMEM;
   } catch (...) {
     fail = CDA_E_NOMEM;
   }
-  if (fail) {  // nothing was copied: every request of the batch fails as it is
-    for (AxisReq* r : batch) r->rc = fail, r->state = kDone, r->cv.notify_one();
+  if (fail) {  // only this caller's request fails; the others stay queued for the next leader
+    q->pending.erase(std::remove(q->pending.begin(), q->pending.end(), self), q->pending.end());
+    self->rc = fail;
+    self->state = kDone;
     hand_over(q);
     return;
   }
+  q->pending.swap(rest);
   q->copy_left = batch.size();
   for (AxisReq* r : batch) {
     r->state = kCopyIn;

@@ -5,7 +5,7 @@
 #   per_axis    same-box A/B of the per-axis seams: $AXIS_LIBS (default libcda.so) and the oracle
 #   swz         rotating A/B of the NMT levels LDS swizzle (libcda.so vs libcda_noswz.so), bench --no-extras
 #   lds         SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS of the bench step for both builds (one PMC pass each)
-#   bench       the default bench line; profile: scripts/profile.sh r06
+#   bench       the default bench line; profile: scripts/profile.sh $TAG; asan: scripts/gpu_asan.sh
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -44,6 +44,9 @@ or driver or release" > gpurun_out/${T}_tests_axis.log 2>&1
     bench)
       timeout -k 10 900 python -u bench.py > gpurun_out/${T}_bench.log 2>&1
       rc=$?; tail -c 400 gpurun_out/${T}_bench.log ;;
+    asan)
+      timeout -k 10 900 bash scripts/gpu_asan.sh > gpurun_out/${T}_asan.log 2>&1
+      rc=$?; tail -3 gpurun_out/${T}_asan.log ;;
     profile)
       timeout -k 10 1000 bash scripts/profile.sh ${T} > gpurun_out/${T}_profile.log 2>&1
       rc=$?; tail -5 gpurun_out/${T}_profile.log ;;

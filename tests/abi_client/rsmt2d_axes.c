@@ -36,6 +36,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #define SHARE 512
 #define NS 29
@@ -564,5 +565,9 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (use_cda) p_cda_free(g_ctx);
-  return 0;
+  /* leave without the exit-time destructors of the HIP runtime (under the host-ASan build the ASan runtime's own
+     checks fire inside them, after every libcda call has returned; tests/abi_client/abi_host_client.c does the same) */
+  fflush(stdout);
+  fflush(stderr);
+  _exit(0);
 }
