@@ -142,7 +142,7 @@ int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t
 
 // ODS of a share plan (square_kernels.hip), one thread per 16-B word; -2: empty plan
 int launch_scatter_cell_runs(const void* d_compact, void* d_dst, const uint32_t* d_dst_cell, const uint32_t* d_pre,
-                             int nruns, uint32_t ncells, hipStream_t s);
+                             int nruns, uint32_t ncells, hipStream_t s, bool same_layout = false);
 int launch_build_ods(const cda_share_segment* d_segs, int nseg, const uint8_t* d_data, const uint32_t* d_reserved,
                      uint32_t nshares, void* d_ods, hipStream_t s);
 

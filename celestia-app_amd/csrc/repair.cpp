@@ -156,8 +156,12 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
     }
   }
   const bool packed = !runs.empty();
+  // a sparse square in page-locked memory (go/cda's pooled slab, cda_host_register): the scatter kernel reads its
+  // present runs over PCIe itself -- no host copy through the staging ring, no upload ahead of the planning
+  const void* zc = packed ? pinned_device_alias(eds, eds_b) : nullptr;
   if (packed) {
-    if ((rc = ensure(c, c->rcompact, packed_cells * CDA_SHARE)) || (rc = ensure(c, c->rruns, run_tab.size() * 4)))
+    if ((!zc && (rc = ensure(c, c->rcompact, packed_cells * CDA_SHARE))) ||
+        (rc = ensure(c, c->rruns, run_tab.size() * 4)))
       return rc;
     if (!dev_ok(c, hipMemcpyAsync(c->rruns.p, run_tab.data(), run_tab.size() * 4, hipMemcpyHostToDevice, s), "H2D") ||
         !dev_ok(c, hipMemsetAsync(d_eds, 0, eds_b, s), "memset"))
@@ -165,7 +169,7 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   }
   bool h2d_ok = true;
   std::thread h2d;
-  if (eds)
+  if (eds && !zc)
     h2d = std::thread([&] {
       try {
         (void)hipSetDevice(c->device);
@@ -236,7 +240,8 @@ static int repair_impl(cda_ctx* c, uint32_t k, uint8_t* eds, uint8_t* d_eds_in, 
   if (packed) {
     const uint32_t* d_tab = (const uint32_t*)c->rruns.p;
     const int nr = (int)runs.size();
-    if (launch_scatter_cell_runs(c->rcompact.p, d_eds, d_tab, d_tab + nr, nr, (uint32_t)packed_cells, s))
+    if (launch_scatter_cell_runs(zc ? zc : c->rcompact.p, d_eds, d_tab, d_tab + nr, nr, (uint32_t)packed_cells, s,
+                                 zc != nullptr))
       return CDA_E_DEVICE;
   }
   const int* d_ax = (const int*)(dd + o_ax);

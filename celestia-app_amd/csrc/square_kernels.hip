@@ -87,7 +87,9 @@ int launch_build_ods(const cda_share_segment* d_segs, int nseg, const uint8_t* d
 
 // Runs of 512-B cells packed back to back in `compact` (run i = cells [pre[i], pre[i+1]) of the packed stream)
 // go to cell dst_cell[i] onward of `dst`: cda_repair's upload of only the present cells.  One thread per 16-B
-// word, the run found by binary search over pre (nruns + 1 entries).
+// word, the run found by binary search over pre (nruns + 1 entries).  SAME: `compact` is the caller's whole square
+// in page-locked host memory (its device alias), laid out like `dst`; the runs are read straight from it over PCIe.
+template <bool SAME>
 __global__ void __launch_bounds__(256) scatter_cell_runs_kernel(const uint4* __restrict__ compact,
                                                                 uint4* __restrict__ dst,
                                                                 const uint32_t* __restrict__ dst_cell,
@@ -102,16 +104,21 @@ __global__ void __launch_bounds__(256) scatter_cell_runs_kernel(const uint4* __r
     if (pre[mid] <= cell) lo = mid;
     else hi = mid - 1;
   }
-  dst[((size_t)dst_cell[lo] + (cell - pre[lo])) * 32 + (t & 31)] = compact[t];
+  const size_t w = ((size_t)dst_cell[lo] + (cell - pre[lo])) * 32 + (t & 31);
+  dst[w] = compact[SAME ? w : t];
 }
 
 int launch_scatter_cell_runs(const void* d_compact, void* d_dst, const uint32_t* d_dst_cell, const uint32_t* d_pre,
-                             int nruns, uint32_t ncells, hipStream_t s) {
+                             int nruns, uint32_t ncells, hipStream_t s, bool same_layout) {
   if (nruns <= 0 || ncells == 0) return 0;
   if (ncells > (1u << 26)) return -2;
   const uint32_t nwords = ncells * 32;
-  hipLaunchKernelGGL(scatter_cell_runs_kernel, dim3((nwords + 255) / 256), dim3(256), 0, s, (const uint4*)d_compact,
-                     (uint4*)d_dst, d_dst_cell, d_pre, nruns, nwords);
+  if (same_layout)
+    hipLaunchKernelGGL(scatter_cell_runs_kernel<true>, dim3((nwords + 255) / 256), dim3(256), 0, s,
+                       (const uint4*)d_compact, (uint4*)d_dst, d_dst_cell, d_pre, nruns, nwords);
+  else
+    hipLaunchKernelGGL(scatter_cell_runs_kernel<false>, dim3((nwords + 255) / 256), dim3(256), 0, s,
+                       (const uint4*)d_compact, (uint4*)d_dst, d_dst_cell, d_pre, nruns, nwords);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -210,6 +210,24 @@ static bool is_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// The device address of page-locked host memory [p, p + n) when one registered / hipHostMalloc'd range holds all of
+// it (kernels may then read it over PCIe directly), else nullptr.
+const void* pinned_device_alias(const void* p, size_t n) {
+  if (!is_pinned(p)) return nullptr;
+  void* start = nullptr;
+  size_t size = 0;
+  void* d = nullptr;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess ||
+      hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d || !start) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const uintptr_t a = (uintptr_t)p, s0 = (uintptr_t)start;
+  if (a < s0 || a + n > s0 + size) return nullptr;
+  return d;
+}
+
 static bool direct(const cda_ctx* c, const void* host, size_t n, int dir_bit) {
   return !(c->staging & dir_bit) || n < ((size_t)2 << 20) || is_pinned(host);
 }
