@@ -158,15 +158,6 @@ bool consensus_eligible(const cda_ctx* c, uint32_t k) { return c->consensus && !
 
 namespace {
 
-// Page-locked host memory (hipHostMalloc / hipHostRegister)?
-bool pinned_host(const void* p) {
-  hipPointerAttribute_t a{};
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();  // pageable memory is not an error here
-    return false;
-  }
-  return a.type == hipMemoryTypeHost;
-}
 
 int grow_pinned(cda_ctx* c, uint8_t*& p, size_t& cap, size_t need) {
   if (cap >= need) return CDA_OK;
@@ -335,7 +326,7 @@ int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_
       (rc = ensure(c, c->scratch, 2 * cells * CDA_REC_BYTES)) || (rc = prepare_trees(c, k, 1, c->stream)))
     return rc;
   const bool want = eds_or_null != nullptr;
-  const bool out_pinned = want && pinned_host(eds_or_null);
+  const bool out_pinned = want && pinned_range(eds_or_null, eds_b);
   const bool resident = want && !out_pinned && (out_mode == 2 || pages_resident(eds_or_null, eds_b));
   const bool fresh = want && !out_pinned && !resident;
   const bool banded = in_mode_env ? in_mode_env == 1 : want;

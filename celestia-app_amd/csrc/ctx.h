@@ -129,7 +129,8 @@ void free_pipeline(cda_ctx* c);
 // bytes are in h_dst (it waits for s).
 int staged_h2d(cda_ctx* c, void* d_dst, const void* h_src, size_t n, hipStream_t s);
 int staged_d2h(cda_ctx* c, void* h_dst, const void* d_src, size_t n, hipStream_t s);
-// device address of page-locked host memory [p, p + n) inside one registered / pinned range, else nullptr
+// all of [p, p + n) inside one page-locked range (staging.cpp); its device address (or nullptr)
+bool pinned_range(const void* p, size_t n);
 const void* pinned_device_alias(const void* p, size_t n);
 void free_staging(cda_ctx* c);
 // byte range [off, off + len) of a host buffer

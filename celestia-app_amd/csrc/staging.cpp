@@ -210,26 +210,35 @@ static bool is_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// The device address of page-locked host memory [p, p + n) when one registered / hipHostMalloc'd range holds all of
-// it (kernels may then read it over PCIe directly), else nullptr.
-const void* pinned_device_alias(const void* p, size_t n) {
-  if (!is_pinned(p)) return nullptr;
+// Is all of [p, p + n) inside ONE page-locked range (hipHostMalloc'd or registered)?  A DMA or a kernel may then
+// address it directly; a range only partly registered (its start pinned, its end not) fails the DMA engine's
+// translation, so it is pageable here.
+bool pinned_range(const void* p, size_t n) {
+  if (!is_pinned(p)) return false;
   void* start = nullptr;
   size_t size = 0;
-  void* d = nullptr;
   if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
-      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess ||
-      hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d || !start) {
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess || !start) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t a = (uintptr_t)p, s0 = (uintptr_t)start;
+  return a >= s0 && a + n <= s0 + size;
+}
+
+// The device address of page-locked host memory [p, p + n) when one range holds all of it (kernels may then read it
+// over PCIe directly), else nullptr.
+const void* pinned_device_alias(const void* p, size_t n) {
+  void* d = nullptr;
+  if (!pinned_range(p, n) || hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
     (void)hipGetLastError();
     return nullptr;
   }
-  const uintptr_t a = (uintptr_t)p, s0 = (uintptr_t)start;
-  if (a < s0 || a + n > s0 + size) return nullptr;
   return d;
 }
 
 static bool direct(const cda_ctx* c, const void* host, size_t n, int dir_bit) {
-  return !(c->staging & dir_bit) || n < ((size_t)2 << 20) || is_pinned(host);
+  return !(c->staging & dir_bit) || n < ((size_t)2 << 20) || pinned_range(host, n);
 }
 
 int staged_h2d(cda_ctx* c, void* d_dst, const void* h_src, size_t n, hipStream_t s) {

@@ -48,3 +48,20 @@ def test_repair_in_registered_memory_matches_oracle(ctx, case, where):
             assert np.array_equal(square, eds)
     finally:
         ctx.host_unregister(reg)
+
+
+@pytest.mark.parametrize("where", ["whole", "half_registered"])
+def test_one_block_output_in_registered_memory(ctx, where):
+    """The one-block path with its EDS output page-locked whole (one DMA for the bottom half) or only in part (a
+    partly registered range is treated as pageable): bit-exact either way."""
+    k = 128
+    ods = O.gen_ods(k, 0x4242)
+    rc, eds_o, rr_o, cr_o, dah_o = O.extend_commit(ods)
+    out = np.full((1, 4 * k * k, 512), 0x5A, np.uint8)
+    reg = out if where == "whole" else out[0, : 2 * k * k]
+    ctx.host_register(reg)
+    try:
+        _, rr, cr, dah = ctx.extend_commit_batch(ods[None].copy(), eds_out=out)
+        assert np.array_equal(out[0], eds_o) and np.array_equal(rr[0], rr_o) and bytes(dah[0]) == dah_o
+    finally:
+        ctx.host_unregister(reg)
