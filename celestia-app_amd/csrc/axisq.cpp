@@ -261,10 +261,9 @@ bool ensure_host(cda_ctx* c, AxisQueue* q, size_t bytes) {
   (void)hipSetDevice(c->device);
   void* p = nullptr;
   void* d = nullptr;
-  // coherent (fine-grained): the kernels' PCIe reads and writes of this memory are never served from or left in the
-  // GPU's caches, so each batch's inputs are read as the callers wrote them and its results are in host memory when
-  // the stream is synchronised
-  if (hipHostMalloc(&p, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  // coarse-grained page-locked memory: coherent at the points this queue uses it -- the callers write a batch's
+  // inputs before its kernels are launched and read its results after the stream is synchronised
+  if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess ||
       hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
     if (p) (void)hipHostFree(p);
     (void)hipGetLastError();

@@ -198,8 +198,14 @@ __device__ __forceinline__ void ld4(const uint4* p, uint32_t* w) {  // 4 x 16 B 
 // ds_read_b128).  Swizzling the pieces (piece ^ ((lane ^ lane >> 3) & 7)) removed every conflict of the levels 1-2
 // launch (SQ_LDS_BANK_CONFLICT 132 M -> 0) but moved blocks/s by +0.3 / +0.9 % on two boxes (the kernel is
 // VALU-bound): below the 1 % bar, not kept.
+// parity: both children lie in the parity part of the square (every leaf below them has the parity namespace, so each
+// child's first 58 bytes are 0xFF): block 0 is 0x01 ‖ 0xFF x 58 ‖ 5 digest bytes, and its first 14 rounds run on
+// constant words from a constant state -- they are skipped (kParityMid14), 14 of the node's 192 rounds.  About 3 in 4
+// inner nodes of a square are such (rows / columns >= k entirely, the right half of the others).
+constexpr uint32_t kParityMid14[8] = {0xa8abd42b, 0x092979bd, 0x8d5926ca, 0x8df58526,
+                                      0xa812caa9, 0x7cc8da5d, 0x33a85111, 0x7d669380};
 __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, uint4* po, bool store = true,
-                                              uint4* ns_lds = nullptr) {
+                                              uint4* ns_lds = nullptr, bool parity = false) {
   uint32_t st[8], m[16];
   sha256_init(st);
   // message = 0x01 ‖ L[0..90) ‖ R[0..90) ‖ 0x80 ‖ 0.. ‖ len(1448 bits); 48 words
@@ -213,7 +219,20 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
 #pragma unroll
       for (int i = 0; i < 4; i++) ns_lds[i] = make_uint4(L[4 * i], L[4 * i + 1], L[4 * i + 2], L[4 * i + 3]);
   }
-  sha256_compress_fenced(st, m);
+  if (parity) {
+    uint32_t mw[16];
+    mw[0] = 0x01FFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 14; i++) mw[i] = 0xFFFFFFFFu;
+    mw[14] = m[14];
+    mw[15] = m[15];
+    uint32_t mid[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) mid[i] = kParityMid14[i];
+    sha256_compress_fenced_from<14>(st, mid, mw);
+  } else {
+    sha256_compress_fenced(st, m);
+  }
   {  // block 1: words 16..31 <- L words 15..22, R words 0..8
     uint32_t L[16], R[16];  // L words 12..27, R words 0..15
     ld4(launder_after(pl, st[0]) + 3, L);  // words 12..27: only 12..23 are read

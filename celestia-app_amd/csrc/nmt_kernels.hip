@@ -126,12 +126,20 @@ __global__ void __launch_bounds__(256) nmt_levels_kernel(LevelSet ls, int log2w,
   const unsigned tree = col ? (r2 & (w - 1)) : (r2 >> log2n_out);
   const unsigned j = col ? (r2 >> log2w) : (r2 & ((1u << log2n_out) - 1));
   __shared__ uint4 s_ns[256 * 8];  // per thread: the first 64 B of both children of the node being hashed
+  const unsigned k = w >> 1;
+  const int l_in = log2w - log2n_out - M;
   for (int q = 1; q <= M; q++) {
     const unsigned cnt = 1u << (M - q);  // nodes of this subtree at level l_in + q
     for (unsigned t = 0; t < cnt; t++) {
       const unsigned i = j * cnt + t;
+      // every leaf under node i is a parity leaf (axis >= k, or leaves i << level onward all >= k): nmt_dev.h
+#if CDA_NO_PARITY_MID  // diagnostic A/B: every node through the full 64 rounds of block 0
+      const bool parity = false;
+#else
+      const bool parity = tree >= k || (i << (l_in + q)) >= k;
+#endif
       hash_node_mem(level_rec(ls.lv[q - 1], b, col, tree, 2 * i), level_rec(ls.lv[q - 1], b, col, tree, 2 * i + 1),
-                    level_rec(ls.lv[q], b, col, tree, i), true, s_ns + threadIdx.x * 8);
+                    level_rec(ls.lv[q], b, col, tree, i), true, s_ns + threadIdx.x * 8, parity);
     }
     // the next level reads what this thread just stored
     if (q < M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -223,6 +223,48 @@ __device__ __forceinline__ void sha256_compress_fenced(uint32_t s[8], const uint
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// A block whose first START message words are the constants w[0..START) and whose chaining input is s: the 64-round
+// compression started from `mid`, the working state after rounds 0..START-1 (precomputed on the host for the fixed
+// prefix).  The schedule still reads w[0..16) (the constant words fold into it).  s += the final working state.
+template <int START>
+__device__ __forceinline__ void sha256_compress_fenced_from(uint32_t s[8], const uint32_t (&mid)[8],
+                                                            uint32_t (&w)[16]) {
+  uint32_t a = mid[0], b = mid[1], c = mid[2], d = mid[3], e = mid[4], f = mid[5], g = mid[6], h = mid[7];
+#pragma unroll
+  for (int t = START; t < 64; t++) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + K256::v[t] + wt;
+    const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+    if ((t % 8) == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  s[0] += a;
+  s[1] += b;
+  s[2] += c;
+  s[3] += d;
+  s[4] += e;
+  s[5] += f;
+  s[6] += g;
+  s[7] += h;
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Opaque copy of a pointer: loads through it are neither merged with earlier
 // loads of the same address (CSE) nor kept live from them.
 template <typename T>

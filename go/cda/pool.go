@@ -303,11 +303,13 @@ func (x *Context) Trim() {
 			if key.ctx != x {
 				continue
 			}
+			var kept []interface{}
 			for _, arr := range l {
 				b := slabBytes(arr, key.n)
 				if x.c != nil {
 					if rc := C.cda_host_unregister(x.c, unsafe.Pointer(&b[0])); rc != 0 {
-						// still registered: keep the slab (and its count) rather than drop locked pages
+						// still registered: keep the slab in the pool (and its count) rather than drop locked pages
+						kept = append(kept, arr)
 						continue
 					}
 				}
@@ -315,7 +317,11 @@ func (x *Context) Trim() {
 				p.live[key]--
 				stats.dropped.Add(1)
 			}
-			delete(p.free, key)
+			if len(kept) > 0 {
+				p.free[key] = kept
+			} else {
+				delete(p.free, key)
+			}
 		}
 		p.mu.Unlock()
 	}

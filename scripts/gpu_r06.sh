@@ -3,8 +3,7 @@
 #   tests_axis  per-axis seams + codec / tree / consensus-form / fault tests
 #   tests       the whole GPU suite
 #   per_axis    same-box A/B of the per-axis seams: $AXIS_LIBS (default libcda.so) and the oracle
-#   swz         rotating A/B of the NMT levels LDS swizzle (libcda.so vs libcda_noswz.so), bench --no-extras
-#   lds         SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS of the bench step for both builds (one PMC pass each)
+#   ab          rotating same-box A/B of $AB_LIBS (bench --no-extras), $AB_ROUNDS rounds
 #   bench       the default bench line; profile: scripts/profile.sh $TAG; asan: scripts/gpu_asan.sh
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -28,19 +27,10 @@ or driver or release" > gpurun_out/${T}_tests_axis.log 2>&1
       timeout -k 10 900 python -u scripts/per_axis_ab.py ${AXIS_LIBS:-celestia-app_amd/cda/libcda.so} \
         > gpurun_out/${T}_per_axis.json 2> gpurun_out/${T}_per_axis.err
       rc=$?; tail -c 600 gpurun_out/${T}_per_axis.err ;;
-    swz)
-      timeout -k 10 900 bash scripts/ab_bench.sh ${SWZ_ROUNDS:-3} celestia-app_amd/cda/libcda.so \
-        celestia-app_amd/cda/libcda_noswz.so > gpurun_out/${T}_swz_ab.log 2>&1
-      rc=$?; cp gpurun_out/ab_runs.jsonl gpurun_out/${T}_swz_ab_runs.jsonl 2>/dev/null; tail -4 gpurun_out/${T}_swz_ab.log ;;
-    lds)
-      rc=0
-      for lib in libcda libcda_noswz; do
-        (cd /tmp && export TMPDIR=/tmp && CDA_LIB=$R/celestia-app_amd/cda/$lib.so timeout -k 10 300 rocprofv3 \
-          --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES --kernel-trace --output-format csv \
-          -d "$R/gpurun_out/${T}_lds_$lib" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline \
-          --no-extras --no-k512-split > "$R/gpurun_out/${T}_lds_$lib.log" 2>&1)
-        rc=$?; tail -2 "gpurun_out/${T}_lds_$lib.log"; [ $rc -ne 0 ] && break
-      done ;;
+    ab)
+      timeout -k 10 900 bash scripts/ab_bench.sh ${AB_ROUNDS:-3} ${AB_LIBS:-celestia-app_amd/cda/libcda.so} \
+        > gpurun_out/${T}_ab.log 2>&1
+      rc=$?; cp gpurun_out/ab_runs.jsonl gpurun_out/${T}_ab_runs.jsonl 2>/dev/null; tail -4 gpurun_out/${T}_ab.log ;;
     bench)
       timeout -k 10 900 python -u bench.py > gpurun_out/${T}_bench.log 2>&1
       rc=$?; tail -c 400 gpurun_out/${T}_bench.log ;;
