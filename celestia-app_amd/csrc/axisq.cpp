@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -252,20 +253,34 @@ int run_device(cda_ctx* c, const Layout& L, uint8_t* h, uint8_t* hd) {
   return CDA_OK;
 }
 
-bool ensure_host(cda_ctx* c, AxisQueue* q, size_t bytes) {
-  if (q->h_cap >= bytes) return true;
-  const size_t cap = std::max({bytes, (size_t)4 << 20, std::min(2 * q->h_cap, kBatchBytes)});
-  if (q->h) (void)hipHostFree(q->h);
+void free_host(AxisQueue* q) {
+  if (!q->h) return;
+  (void)hipHostUnregister(q->h);
+  free(q->h);
   q->h = q->hd = nullptr;
   q->h_cap = 0;
+}
+
+bool ensure_host(cda_ctx* c, AxisQueue* q, size_t bytes) {
+  if (q->h_cap >= bytes) return true;
+  const size_t cap = (std::max({bytes, (size_t)4 << 20, std::min(2 * q->h_cap, kBatchBytes)}) + 4095) & ~(size_t)4095;
+  free_host(q);
   (void)hipSetDevice(c->device);
   void* p = nullptr;
   void* d = nullptr;
-  // coarse-grained page-locked memory: coherent at the points this queue uses it -- the callers write a batch's
-  // inputs before its kernels are launched and read its results after the stream is synchronised
-  if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess ||
-      hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
-    if (p) (void)hipHostFree(p);
+  // page-aligned host memory page-locked by registration (coarse-grained): coherent at the points this queue uses it
+  // -- the callers write a batch's inputs before its kernels are launched and read its results after the stream is
+  // synchronised.  (Registered rather than hipHostMalloc'd: under the host-ASan build the runtime's interceptor of
+  // the HSA pool allocator refused it from a worker thread, scripts/gpu_asan.sh.)
+  if (posix_memalign(&p, 4096, cap) != 0) return false;
+  if (hipHostRegister(p, cap, hipHostRegisterDefault) != hipSuccess) {
+    free(p);
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+    (void)hipHostUnregister(p);
+    free(p);
     (void)hipGetLastError();
     return false;
   }
@@ -428,7 +443,7 @@ int axis_root_wide(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uint32
 
 void free_axisq(cda_ctx* c) {
   if (!c->axq) return;
-  if (c->axq->h) (void)hipHostFree(c->axq->h);
+  free_host(c->axq);
   delete c->axq;
   c->axq = nullptr;
 }

@@ -38,6 +38,14 @@ __device__ __forceinline__ int ns_cmp(const uint32_t* a, const uint32_t* b) {
   return 0;
 }
 
+// A parity leaf's first block starts 0x00 ‖ 0xFF x 29 (message words 0..6 constant): its working state after rounds
+// 0..6 is a constant, so those rounds are skipped (3 in 4 cells of a square are parity leaves).
+constexpr uint32_t kParityLeafMid7[8] = {0x1ca5c518, 0x33e5c969, 0xbd2d00ce, 0xa4502bae,
+                                         0xce23fa11, 0x90a5b516, 0x5df56d75, 0xf3f677da};
+#ifndef CDA_NO_PARITY_MID
+#define CDA_NO_PARITY_MID 0  // diagnostic A/B: every leaf and inner node through all 64 rounds of its first block
+#endif
+
 // Leaf record of one 512-B share whose first 64 bytes are already in A[0..16):
 // ns ‖ ns ‖ SHA256(0x00 ‖ ns ‖ share) ‖ 6 zero bytes, ns = share[0:29] if q0 else 0xFF×29.
 // Blocks 1..7 stay a loop (one copy of the compression code: measured as fast as
@@ -71,7 +79,21 @@ __device__ __forceinline__ void leaf_record(const uint4* sh, uint32_t* A, bool q
   }
 #pragma unroll
   for (int i = 8; i < 16; i++) m[i] = be_window(A[i - 8], A[i - 7], 2);
-  sha256_compress(st, m);
+  // wave-uniform only (a wave of parity and Q0 cells runs the general path: both paths in one wave cost more than the
+  // 7 rounds saved)
+  if (!CDA_NO_PARITY_MID && __all(!q0)) {
+    uint32_t mw[16], mid[8];
+    mw[0] = 0x00FFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 7; i++) mw[i] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 7; i < 16; i++) mw[i] = m[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) mid[i] = kParityLeafMid7[i];
+    sha256_compress_fenced_from<7, false>(st, mid, mw);
+  } else {
+    sha256_compress(st, m);
+  }
   // blocks 1..7: message words 16j..16j+15 = share bytes 64j-30.. : windows of S[16j-8 .. 16j+8].
   // H carries the upper half of the previous 16-word chunk.
   uint32_t H[8];
@@ -219,7 +241,9 @@ __device__ __forceinline__ void hash_node_mem(const uint4* pl, const uint4* pr, 
 #pragma unroll
       for (int i = 0; i < 4; i++) ns_lds[i] = make_uint4(L[4 * i], L[4 * i + 1], L[4 * i + 2], L[4 * i + 3]);
   }
-  if (parity) {
+  // wave-uniform only: a wave whose nodes are partly parity takes the general path (in a divergent wave both paths
+  // would run, 114 rounds instead of 64; measured 3 % slower on the step, profiles/r06_ab_parity_mid.jsonl)
+  if (__all(parity)) {
     uint32_t mw[16];
     mw[0] = 0x01FFFFFFu;
 #pragma unroll

@@ -226,7 +226,7 @@ __device__ __forceinline__ void sha256_compress_fenced(uint32_t s[8], const uint
 // A block whose first START message words are the constants w[0..START) and whose chaining input is s: the 64-round
 // compression started from `mid`, the working state after rounds 0..START-1 (precomputed on the host for the fixed
 // prefix).  The schedule still reads w[0..16) (the constant words fold into it).  s += the final working state.
-template <int START>
+template <int START, bool FENCED = true>
 __device__ __forceinline__ void sha256_compress_fenced_from(uint32_t s[8], const uint32_t (&mid)[8],
                                                             uint32_t (&w)[16]) {
   uint32_t a = mid[0], b = mid[1], c = mid[2], d = mid[3], e = mid[4], f = mid[5], g = mid[6], h = mid[7];
@@ -252,7 +252,7 @@ __device__ __forceinline__ void sha256_compress_fenced_from(uint32_t s[8], const
     c = b;
     b = a;
     a = t1 + t2;
-    if ((t % 8) == 7) __builtin_amdgcn_sched_barrier(0);
+    if (FENCED && (t % 8) == 7) __builtin_amdgcn_sched_barrier(0);
   }
   s[0] += a;
   s[1] += b;
@@ -262,7 +262,7 @@ __device__ __forceinline__ void sha256_compress_fenced_from(uint32_t s[8], const
   s[5] += f;
   s[6] += g;
   s[7] += h;
-  __builtin_amdgcn_sched_barrier(0);
+  if (FENCED) __builtin_amdgcn_sched_barrier(0);
 }
 
 // Opaque copy of a pointer: loads through it are neither merged with earlier

@@ -59,3 +59,14 @@ def test_finishing_from_the_midstate_is_the_compression(seed):
     tail = os.urandom(5) if seed else bytes(5)
     w = schedule(b"\x01" + b"\xff" * 58 + tail)
     assert rounds(kernel_constant(), w, 14, 64) == rounds(IV, w, 0, 64)
+
+
+def test_parity_leaf_midstate_constant():
+    """kParityLeafMid7: a parity leaf's first block is 0x00 ‖ 0xFF x 29 ‖ share[0..34); rounds 0..6 are constant."""
+    src = open(os.path.join(ROOT, "celestia-app_amd", "csrc", "nmt_dev.h")).read()
+    body = re.search(r"kParityLeafMid7\[8\] = \{([^}]*)\}", src).group(1)
+    mid = [int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]+", body)]
+    share_head = os.urandom(34)
+    w = schedule(b"\x00" + b"\xff" * 29 + share_head)
+    assert mid == rounds(IV, w, 0, 7)
+    assert rounds(mid, w, 7, 64) == rounds(IV, w, 0, 64)
