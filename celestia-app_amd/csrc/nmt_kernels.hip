@@ -864,6 +864,9 @@ int launch_axes_verify(const uint8_t* d_eds, int k, const int* d_axes, int ntree
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// trees of at most this many leaves also run a level of 65..128 nodes through the latency path (LDS for 2 x 128 rows)
+constexpr int kAxisRootsKw128MaxLeaves = 512;
+
 // Roots of independent wrapper trees handed over through the per-axis seam (ErasuredNamespacedMerkleTree Push x n +
 // Root, pkg/wrapper/nmt_wrapper.go:93-124; axisq.cpp coalesces concurrent calls into one launch).  Tree t's n leaves
 // are contiguous 512-B shares at leaves + t * tree_stride; its axis index axis_idx[t] and the square size give the
@@ -877,8 +880,9 @@ __global__ void __launch_bounds__(256) axis_roots_kernel(const uint8_t* __restri
                                                          const unsigned long long* __restrict__ axis_idx,
                                                          uint4* __restrict__ roots,
                                                          unsigned long long* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) uint4 lnodes[];  // [n][6]
+  extern __shared__ __attribute__((aligned(16))) uint4 lnodes[];  // [n][6], then 2 x 64 (or 128) K+W schedule rows
   __shared__ unsigned bad;
+  uint32_t* kw = reinterpret_cast<uint32_t*>(lnodes + (size_t)n * 6);
   const int t = blockIdx.x;
   const unsigned long long axis = axis_idx[t];
   const uint8_t* base = leaves + (size_t)t * tree_stride;
@@ -902,14 +906,53 @@ __global__ void __launch_bounds__(256) axis_roots_kernel(const uint8_t* __restri
   for (int c = n; c > 1; c = (c + 1) >> 1) {
     l++;
     const int pairs = c >> 1;
-    if (pairs >= 64) {
+    // round lanes of the latency path: 64 (one wave), or 128 for a level of 65..128 nodes when LDS holds the rows
+    const int nr = pairs <= 64 ? 64 : 128;
+    if (pairs > 128 || (nr == 128 && n > kAxisRootsKw128MaxLeaves)) {
       for (int i = threadIdx.x; i < pairs; i += blockDim.x)
         hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
                       lnodes + ((size_t)i << l) * 6);
-    } else if (threadIdx.x < 64) {  // a small level: the whole wave computes (lanes past the last pair store nothing)
-      const int i = (int)threadIdx.x < pairs ? (int)threadIdx.x : 0;
-      hash_node_mem(lnodes + ((size_t)(2 * i) << (l - 1)) * 6, lnodes + ((size_t)(2 * i + 1) << (l - 1)) * 6,
-                    lnodes + ((size_t)i << l) * 6, (int)threadIdx.x < pairs);
+    } else {
+      // a level of <= 64 nodes is the tree's latency chain (one wave per node set, ~5.4 cycles per instruction):
+      // wave 0 hashes block 0 of its node while wave 1 expands the K+W schedules of blocks 1 and 2, and after the
+      // barrier wave 0 runs only those two blocks' rounds (as trees_lds_kernel; lanes past the last pair hash node 0
+      // again and store nothing, with full exec masks)
+      const int i = (int)threadIdx.x & (nr - 1);
+      const int p = i < pairs ? i : 0;
+      uint32_t L[24], R[24], st[8];
+      if ((int)threadIdx.x < 2 * nr) {
+        const uint4* pl = lnodes + ((size_t)(2 * p) << (l - 1)) * 6;
+        const uint4* pr = lnodes + ((size_t)(2 * p + 1) << (l - 1)) * 6;
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+          const uint4 u = pl[q], v = pr[q];
+          L[4 * q] = u.x, L[4 * q + 1] = u.y, L[4 * q + 2] = u.z, L[4 * q + 3] = u.w;
+          R[4 * q] = v.x, R[4 * q + 1] = v.y, R[4 * q + 2] = v.z, R[4 * q + 3] = v.w;
+        }
+        uint32_t m[16];
+        if ((int)threadIdx.x < nr) {
+          sha256_init(st);
+          node_block<0>(L, R, m);
+          sha256_compress(st, m);
+        } else {
+          node_block<1>(L, R, m);
+          sha256_kw_store(m, kw + i * kKwStride);
+          node_block<2>(L, R, m);
+          sha256_kw_store(m, kw + (nr + i) * kKwStride);
+        }
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < nr) {
+        sha256_rounds_kw(st, kw + i * kKwStride);
+        sha256_rounds_kw(st, kw + (nr + i) * kKwStride);
+        uint32_t o[24];
+        node_record(L, R, st, o);
+        if (i < pairs) {
+          uint4* po = lnodes + ((size_t)i << l) * 6;
+#pragma unroll
+          for (int q = 0; q < 6; q++) po[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        }
+      }
     }
     __syncthreads();
   }
@@ -922,7 +965,7 @@ int launch_axis_roots(const uint8_t* d_leaves, long long tree_stride, int n, uin
                       hipStream_t s) {
   if (ntrees <= 0) return 0;
   if (n < 1 || n > kAxisRootsMaxLeaves) return -2;
-  const size_t lds = (size_t)n * CDA_REC_BYTES;
+  const size_t lds = (size_t)n * CDA_REC_BYTES + (size_t)2 * (n <= kAxisRootsKw128MaxLeaves ? 128 : 64) * kKwStride * 4;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute((const void*)axis_roots_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
           hipSuccess)
