@@ -55,6 +55,8 @@ static void (*p_cda_free)(void*);
 static int (*p_cda_rs_encode)(void*, uint32_t, uint32_t, const uint8_t*, uint8_t*);
 static int (*p_cda_rs_decode)(void*, uint32_t, uint32_t, uint8_t*, const uint8_t*);
 static int (*p_cda_nmt_axis_root)(void*, uint64_t, uint64_t, uint32_t, uint32_t, const uint8_t*, uint8_t*, err_info*);
+static int (*p_cda_profile_enable)(void*, int);
+static int (*p_cda_profile_read)(void*, char*, size_t, double*, int64_t*, int);
 /* oracle */
 static int (*p_ora_encode)(int, size_t, const uint8_t* const*, uint8_t* const*);
 static int (*p_ora_decode)(int, size_t, uint8_t* const*, const uint8_t*);
@@ -84,6 +86,8 @@ static void load_backend(const char* kind, const char* path) {
     *(void**)&p_cda_rs_encode = sym(h, "cda_rs_encode");
     *(void**)&p_cda_rs_decode = sym(h, "cda_rs_decode");
     *(void**)&p_cda_nmt_axis_root = sym(h, "cda_nmt_axis_root");
+    *(void**)&p_cda_profile_enable = sym(h, "cda_profile_enable");
+    *(void**)&p_cda_profile_read = sym(h, "cda_profile_read");
     if (p_cda_init(0, &g_ctx) != 0) {
       fprintf(stderr, "cda_init failed\n");
       exit(2);
@@ -457,7 +461,26 @@ static void mode_single(int k, int reps, const uint8_t* ods) {
          "\"root0\": \"",
          1e6 * r[0][0], 1e6 * r[0][1], 1e6 * r[1][0], 1e6 * r[1][1], 1e6 * r[2][0], 1e6 * r[2][1], reps);
   for (int i = 0; i < NODE; i++) printf("%02x", rt[i]);
-  printf("\"}\n");
+  printf("\"");
+  if (use_cda) {  /* the device share of each call: the same calls again with libcda's per-launch HIP events */
+    p_cda_profile_enable(g_ctx, 1);
+    for (int i = 0; i < 50; i++) {
+      if (enc(k, data, par) || dec(k, sh, pres) || root(k, 0, sh, rt)) exit(3);
+    }
+    char names[1024];
+    double ms[16];
+    int64_t cnt[16];
+    const int nk = p_cda_profile_read(g_ctx, names, sizeof names, ms, cnt, 16);
+    p_cda_profile_enable(g_ctx, 0);
+    printf(", \"kernel_us\": {");
+    const char* nm = names;
+    for (int i = 0; i < nk; i++) {
+      printf("%s\"%s\": %.1f", i ? ", " : "", nm, 1e3 * ms[i] / (double)(cnt[i] ? cnt[i] : 1));
+      nm += strlen(nm) + 1;
+    }
+    printf("}");
+  }
+  printf("}\n");
 }
 
 static void mode_extend(int k, int threads, int reps, const uint8_t* ods, const char* out) {
