@@ -866,6 +866,70 @@ int launch_axes_verify(const uint8_t* d_eds, int k, const int* d_axes, int ntree
 
 // trees of at most this many leaves also run a level of 65..128 nodes through the latency path (LDS for 2 x 128 rows)
 constexpr int kAxisRootsKw128MaxLeaves = 512;
+// trees of at most this many leaves hash their leaves in the pipelined form (512 threads, below)
+constexpr int kAxisRootsPipeLeaves = 256;
+
+// Message block j (1..8) of a leaf: 0x00 ‖ ns ‖ share, so block j >= 1 holds share bytes 64j - 30 .. 64j + 33
+// (windows of share words 16j - 8 .. 16j + 8); block 8 ends the 542-byte message (leaf_record's blocks 1..8).
+__device__ __forceinline__ void leaf_block_words(const uint4* sh, int j, uint32_t (&m)[16]) {
+  uint32_t H[8];
+  {
+    const uint4 a = sh[4 * j - 2], b = sh[4 * j - 1];  // share words 16j - 8 .. 16j - 1
+    H[0] = a.x, H[1] = a.y, H[2] = a.z, H[3] = a.w, H[4] = b.x, H[5] = b.y, H[6] = b.z, H[7] = b.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 7; i++) m[i] = be_window(H[i], H[i + 1], 2);
+  if (j < 8) {
+    uint32_t C[16];
+    load16(sh + 4 * j, C);
+    m[7] = be_window(H[7], C[0], 2);
+#pragma unroll
+    for (int i = 8; i < 16; i++) m[i] = be_window(C[i - 8], C[i - 7], 2);
+  } else {
+    m[7] = be_window(H[7], 0x80u, 2);
+#pragma unroll
+    for (int i = 8; i < 15; i++) m[i] = 0;
+    m[15] = 542u * 8u;
+  }
+}
+
+// Block 0 of a leaf from its first 64 share bytes A (leaf_record's block 0; ns = share[0:29] if q0, else 0xFF x 29)
+__device__ __forceinline__ void leaf_block0_words(const uint32_t (&A)[16], bool q0, uint32_t (&m)[16]) {
+  if (q0) {
+    m[0] = be_window(0u, A[0], 3);
+#pragma unroll
+    for (int i = 1; i < 7; i++) m[i] = be_window(A[i - 1], A[i], 3);
+    m[7] = (be_window(A[6], A[7], 3) & 0xFFFF0000u) | (bswap(A[0]) >> 16);
+  } else {
+    m[0] = 0x00FFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 7; i++) m[i] = 0xFFFFFFFFu;
+    m[7] = 0xFFFF0000u | (bswap(A[0]) >> 16);
+  }
+#pragma unroll
+  for (int i = 8; i < 16; i++) m[i] = be_window(A[i - 8], A[i - 7], 2);
+}
+
+// The 96-B leaf record ns ‖ ns ‖ digest ‖ 6 zero bytes from the final state (leaf_record's tail)
+__device__ __forceinline__ void leaf_record_out(const uint32_t (&A)[16], bool q0, const uint32_t (&st)[8], uint4* out) {
+  uint32_t ns[8], d[8], o[24];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ns[i] = q0 ? A[i] : 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = bswap(st[i]);
+#pragma unroll
+  for (int i = 0; i < 7; i++) o[i] = ns[i];
+  o[7] = (ns[7] & 0xFFu) | (ns[0] << 8);
+#pragma unroll
+  for (int i = 8; i < 14; i++) o[i] = le_window(ns[i - 8], ns[i - 7], 3);
+  o[14] = (le_window(ns[6], ns[7], 3) & 0xFFFFu) | (d[0] << 16);
+#pragma unroll
+  for (int i = 15; i < 22; i++) o[i] = le_window(d[i - 15], d[i - 14], 2);
+  o[22] = d[7] >> 16;
+  o[23] = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) out[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
 
 // Roots of independent wrapper trees handed over through the per-axis seam (ErasuredNamespacedMerkleTree Push x n +
 // Root, pkg/wrapper/nmt_wrapper.go:93-124; axisq.cpp coalesces concurrent calls into one launch).  Tree t's n leaves
@@ -875,31 +939,83 @@ constexpr int kAxisRootsKw128MaxLeaves = 512;
 // last odd node keeps its slot, which is the nmt split at the largest power of two below n), the root record to
 // roots[t] and the first leaf whose Push order check fails (nmt ErrInvalidPushOrder) to status[t] (~0 when none).
 // Replaces the leaf launch + ceil(log2 n) level launches of the generic single-tree path.
-__global__ void __launch_bounds__(256) axis_roots_kernel(const uint8_t* __restrict__ leaves, long long tree_stride,
-                                                         int n, unsigned long long square_size,
-                                                         const unsigned long long* __restrict__ axis_idx,
-                                                         uint4* __restrict__ roots,
-                                                         unsigned long long* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) uint4 lnodes[];  // [n][6], then 2 x 64 (or 128) K+W schedule rows
+// PIPE (n <= kAxisRootsPipeLeaves, 512 threads): the leaves' 9 compressions are the other half of the tree's latency
+// chain, so waves 4-7 expand each leaf's next block's K+W schedule into LDS while waves 0-3 run the current block's
+// rounds alone (block 0 in full, then 8 x the 64 rounds: ~8,600 instead of ~13,000 instructions per leaf, double-
+// buffered schedule rows, a barrier per block).  LDS: schedule rows A | B (2 x 256 x kKwStride words); the records
+// go to region B after the last block (block 8's rows are in A), and the levels' schedule rows reuse A.
+template <bool PIPE>
+__global__ void __launch_bounds__(PIPE ? 512 : 256) axis_roots_kernel(const uint8_t* __restrict__ leaves,
+                                                                      long long tree_stride, int n,
+                                                                      unsigned long long square_size,
+                                                                      const unsigned long long* __restrict__ axis_idx,
+                                                                      uint4* __restrict__ roots,
+                                                                      unsigned long long* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_axis[];
   __shared__ unsigned bad;
-  uint32_t* kw = reinterpret_cast<uint32_t*>(lnodes + (size_t)n * 6);
+  constexpr int kRows = kAxisRootsPipeLeaves * kKwStride;  // words of one schedule buffer (PIPE)
+  uint32_t* const kwA = reinterpret_cast<uint32_t*>(lds_axis);
+  // records: [n][6] (after the schedule buffer A and inside B when PIPE); then the levels' 2 x 64 (or 128) rows
+  uint4* const lnodes = PIPE ? reinterpret_cast<uint4*>(kwA + kRows) : lds_axis;
+  uint32_t* kw = PIPE ? kwA : reinterpret_cast<uint32_t*>(lnodes + (size_t)n * 6);
   const int t = blockIdx.x;
   const unsigned long long axis = axis_idx[t];
   const uint8_t* base = leaves + (size_t)t * tree_stride;
   if (threadIdx.x == 0) bad = 0xFFFFFFFFu;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const bool q0 = (unsigned long long)i < square_size && axis < square_size;
-    const uint4* sh = reinterpret_cast<const uint4*>(base + (size_t)i * CDA_SHARE);
-    uint32_t A[16];
-    load16(sh, A);
-    if (q0 && (unsigned long long)(i + 1) < square_size && i + 1 < n) {
-      const uint4* p = sh + CDA_SHARE / 16;
-      const uint4 v0 = p[0], v1 = p[1];
-      uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (ns_cmp(nb, A) < 0) atomicMin(&bad, (unsigned)(i + 1));
+  if (PIPE) {
+    const bool rounds = threadIdx.x < kAxisRootsPipeLeaves;
+    const int i = (int)threadIdx.x & (kAxisRootsPipeLeaves - 1);
+    const int li = i < n ? i : 0;  // lanes past the last leaf hash leaf 0 again and store nothing
+    const bool q0 = (unsigned long long)li < square_size && axis < square_size;
+    const uint4* sh = reinterpret_cast<const uint4*>(base + (size_t)li * CDA_SHARE);
+    uint32_t A[16], st[8];
+    uint32_t* const kwB = kwA + kRows;
+    if (rounds) {
+      load16(sh, A);
+      if (i < n && q0 && (unsigned long long)(i + 1) < square_size && i + 1 < n) {
+        const uint4* p = sh + CDA_SHARE / 16;
+        const uint4 v0 = p[0], v1 = p[1];
+        uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (ns_cmp(nb, A) < 0) atomicMin(&bad, (unsigned)(i + 1));
+      }
+      uint32_t m[16];
+      leaf_block0_words(A, q0, m);
+      sha256_init(st);
+      sha256_compress(st, m);
+    } else {
+      uint32_t m[16];
+      leaf_block_words(sh, 1, m);
+      sha256_kw_store(m, kwB + i * kKwStride);
     }
-    leaf_record<false>(sh, A, q0, lnodes + (size_t)i * 6);
+    __syncthreads();
+    for (int j = 1; j <= 8; j++) {
+      uint32_t* cur = (j & 1) ? kwB : kwA;
+      uint32_t* nxt = (j & 1) ? kwA : kwB;
+      if (rounds) {
+        sha256_rounds_kw(st, cur + i * kKwStride);
+      } else if (j < 8) {
+        uint32_t m[16];
+        leaf_block_words(sh, j + 1, m);
+        sha256_kw_store(m, nxt + i * kKwStride);
+      }
+      __syncthreads();
+    }
+    if (rounds && i < n) leaf_record_out(A, q0, st, lnodes + (size_t)i * 6);
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const bool q0 = (unsigned long long)i < square_size && axis < square_size;
+      const uint4* sh = reinterpret_cast<const uint4*>(base + (size_t)i * CDA_SHARE);
+      uint32_t A[16];
+      load16(sh, A);
+      if (q0 && (unsigned long long)(i + 1) < square_size && i + 1 < n) {
+        const uint4* p = sh + CDA_SHARE / 16;
+        const uint4 v0 = p[0], v1 = p[1];
+        uint32_t nb[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (ns_cmp(nb, A) < 0) atomicMin(&bad, (unsigned)(i + 1));
+      }
+      leaf_record<false>(sh, A, q0, lnodes + (size_t)i * 6);
+    }
   }
   __syncthreads();
   int l = 0;
@@ -965,12 +1081,21 @@ int launch_axis_roots(const uint8_t* d_leaves, long long tree_stride, int n, uin
                       hipStream_t s) {
   if (ntrees <= 0) return 0;
   if (n < 1 || n > kAxisRootsMaxLeaves) return -2;
+  if (n <= kAxisRootsPipeLeaves) {  // the schedule buffers hold the levels' rows and the records (B) as well
+    const size_t lds = (size_t)2 * kAxisRootsPipeLeaves * kKwStride * 4;
+    if (hipFuncSetAttribute((const void*)axis_roots_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(axis_roots_kernel<true>, dim3(ntrees), dim3(512), lds, s, d_leaves, tree_stride, n,
+                       (unsigned long long)square_size, d_axis_idx, (uint4*)d_roots, d_status);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   const size_t lds = (size_t)n * CDA_REC_BYTES + (size_t)2 * (n <= kAxisRootsKw128MaxLeaves ? 128 : 64) * kKwStride * 4;
   if (lds > 64 * 1024 &&
-      hipFuncSetAttribute((const void*)axis_roots_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-          hipSuccess)
+      hipFuncSetAttribute((const void*)axis_roots_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
     return -1;
-  hipLaunchKernelGGL(axis_roots_kernel, dim3(ntrees), dim3(256), lds, s, d_leaves, tree_stride, n,
+  hipLaunchKernelGGL(axis_roots_kernel<false>, dim3(ntrees), dim3(256), lds, s, d_leaves, tree_stride, n,
                      (unsigned long long)square_size, d_axis_idx, (uint4*)d_roots, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
