@@ -135,8 +135,11 @@ int cda_host_free(cda_ctx* ctx, void* p);
 /* Page-lock caller memory for reuse as share / EDS buffers (hipHostRegister): go/cda's buffer pools register Go-heap
  * slabs once and recycle them through the garbage collector, so the consensus path's copies are direct DMAs
  * (app/prepare_proposal.go:65, app/process_proposal.go:137, app/extend_block.go:25 through da.ExtendShares).
- * Unregister only after the last call that used the range has returned (unregister waits for this context's
- * stream first). */
+ * The runtime keeps the registered address after this call returns.  For Go memory that stretches cgo's rule that C
+ * keeps no Go pointer: it is sound only because the gc toolchain's heap never moves an object (go/cda/pool.go states
+ * the invariant; a slab is unregistered before the pool drops it and never freed while registered).  Unregister only
+ * after the last call that used the range has returned (unregister first drains this context's compute, H2D, D2H
+ * and auxiliary streams). */
 int cda_host_register(cda_ctx* ctx, void* p, size_t bytes);
 int cda_host_unregister(cda_ctx* ctx, void* p);
 
