@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B/... of library builds on one box: short bench runs (no extras) in a rotating order so that run position
 # (clock / thermal drift) does not favour one build; prints each run and the per-build means of the kernel times.
-# usage: scripts/ab_bench.sh <rounds> <lib.so> [<lib.so> ...]
+# usage: scripts/ab_bench.sh <rounds> <lib.so>[@VAR=value] [<lib.so>[@VAR=value] ...]
+#   (lib.so@VAR=value: that build with VAR=value in the environment, for the knobs of the hooks build)
 set -u
 N=$1; shift
 LIBS=("$@")
@@ -11,7 +12,8 @@ mkdir -p gpurun_out
 for i in $(seq 0 $((N - 1))); do
   for j in $(seq 0 $((M - 1))); do
     lib=${LIBS[$(((i + j) % M))]}
-    CDA_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-k512-split > gpurun_out/ab_run.log 2>&1 || exit 1
+    path=${lib%%@*}; envs=(); [ "$path" != "$lib" ] && envs=("${lib#*@}")
+    env "${envs[@]}" CDA_LIB=$path timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-k512-split > gpurun_out/ab_run.log 2>&1 || exit 1
     python3 -c "
 import json
 for l in open('gpurun_out/ab_run.log'):
