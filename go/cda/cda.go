@@ -3,9 +3,10 @@
 // Package cda binds libcda.so (include/cda.h), the MI355X data-availability engine, into celestia-app.
 //
 // It keeps the reference's call surface:
-//   - Codec implements rsmt2d.Codec (Encode / Decode / MaxChunks / Name / ValidateChunkSize) and replaces
-//     rsmt2d.NewLeoRSCodec behind appconsts.DefaultCodec (pkg/appconsts/global_consts.go:92, after the
-//     one-line retype in ../patches/0001-appconsts-DefaultCodec-codec-interface.patch);
+//   - Codec implements rsmt2d.Codec (Encode / Decode / MaxChunks / Name / ValidateChunkSize); a caller may opt in to
+//     it behind appconsts.DefaultCodec (pkg/appconsts/global_consts.go:92, after the one-line retype in
+//     ../patches/0001-appconsts-DefaultCodec-codec-interface.patch).  The rocm build does not: per axis the GPU
+//     does not beat the CPU codec (INTEGRATION.md §2), so only the whole-square operations below go to the GPU;
 //   - NewConstructor is an rsmt2d.TreeConstructorFn with wrapper.NewConstructor's semantics
 //     (pkg/wrapper/nmt_wrapper.go:73-140) whose Root() hashes on the GPU;
 //   - ExtendShares has da.ExtendShares' signature (pkg/da/data_availability_header.go:65-75) and returns an
