@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — ODS -> EDS + 4k NMT roots + DAH throughput on MI355X.
 
-Metric (BASELINE.json): "ODS->EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s".
+Metric (BASELINE.json): "ODS\u2192EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s".
 A step = one pass of the hot path (da.ExtendShares + NewDataAvailabilityHeader
 restated: RS rows, RS columns, leaf hashing, NMT levels, DAH) over a batch of B
 independent k=128 blocks per GPU, inputs already resident in HBM.  N GPUs shard
@@ -1272,7 +1272,7 @@ def bench_main(args, world, rank, local, helper):
     comp_per_s = block_compressions_engine(k) * value / world
 
     result = {
-        "metric": "ODS->EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s",
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "blocks/s",
         "n_gpus": world,
@@ -1338,6 +1338,8 @@ def bench_main(args, world, rank, local, helper):
         dist.destroy_process_group()
 
 
+# BASELINE.json's metric, verbatim (the driver matches the line against it)
+METRIC = "ODS\u2192EDS+DAH blocks/sec at k=128 (1/8 GPU); achieved HBM GB/s"
 DISTINCT_ODS = 16  # distinct synthetic squares per rank (tests/golden/make_bench_digests.py covers ranks 0..7)
 
 
