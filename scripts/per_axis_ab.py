@@ -11,12 +11,20 @@ import bench  # noqa: E402
 
 libs = sys.argv[1:] or [os.path.join(ROOT, "celestia-app_amd", "cda", "libcda.so")]
 out = {}
-for lib in libs:
+for arg in libs:  # lib.so or lib.so@VAR=value (a knob of the test-hooks build, set for that run only)
+    lib, _, assign = arg.partition("@")
+    name = os.path.basename(lib) + (f"@{assign}" if assign else "")
+    var, _, val = assign.partition("=")
+    if var:
+        os.environ[var] = val
     try:
-        out[os.path.basename(lib)] = bench.per_axis_measure("cda", lib)
+        out[name] = bench.per_axis_measure("cda", lib)
     except Exception as e:  # noqa: BLE001
-        out[os.path.basename(lib)] = {"error": f"{type(e).__name__}: {e}"}
-    print(json.dumps({os.path.basename(lib): out[os.path.basename(lib)]}), flush=True)
+        out[name] = {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        if var:
+            del os.environ[var]
+    print(json.dumps({name: out[name]}), flush=True)
 out["oracle"] = bench.per_axis_measure("oracle", os.path.join(ROOT, "oracle", "liboracle.so"), reps=3, reps_repair=2,
                                        reps_single=100)
 print(json.dumps(out), flush=True)

@@ -785,7 +785,7 @@ ctx = cda.Context(0)
 dev = torch.device("cuda", 0)
 rng = np.random.default_rng(7)
 for k, ncw, L in [(16, 4, 512), (17, 4, 512), (34, 6, 512), (64, 2, 1024), (100, 4, 512), (128, 6, 512),
-                  (128, 3, 512), (126, 2, 512)]:
+                  (128, 3, 512), (126, 2, 512), (128, 65, 512), (64, 63, 512), (32, 101, 1024), (100, 33, 512)]:
     data = rng.integers(0, 256, (ncw, k, L), dtype=np.uint8)
     d_src = torch.from_numpy(data).to(dev)
     d_dst = torch.zeros((ncw, k, L), dtype=torch.uint8, device=dev)
@@ -810,8 +810,8 @@ print("rs device ok")
 
 def test_rs_encode_device_batched_strided():
     """cda_rs_encode_device, the batched strided Codec.Encode of the split path: even k (register encoder, incl.
-    non-powers of two whose padded elements are zero), odd k and odd codeword counts (LDS encoder), row- and
-    column-strided codewords, each codeword equal to the oracle's Leopard encode."""
+    non-powers of two whose padded elements are zero), odd k and odd codeword counts up to 101 (LDS encoder), row-
+    and column-strided codewords, each codeword equal to the oracle's Leopard encode."""
     import os
     import subprocess
     import sys
