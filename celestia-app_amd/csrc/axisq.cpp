@@ -8,11 +8,13 @@
 // to the device on its own paid a pageable H2D, one or more launches, a pageable D2H and a synchronisation, and
 // concurrent calls queued behind the context mutex one round trip at a time.  Here every call is a request on the
 // context's axis queue (group commit):
-//   * the first caller that finds no batch in flight becomes the leader and takes every request queued so far (up to
-//     kBatchBytes of staging); requests that arrive while a batch runs form the next one, so a lone caller pays no
-//     wait and concurrent callers share launches;
-//   * each caller copies its own input into the leader's page-locked staging slot and its own output back (the
-//     copies run on the callers' threads in parallel), so the device sees one H2D and one D2H per batch;
+//   * a caller that finds a free batch slot becomes a leader and takes every request queued so far (up to
+//     kBatchBytes of staging); requests that arrive while every slot is busy form the next batch, so a lone caller
+//     pays no wait and concurrent callers share launches.  Up to kSlots batches are in flight at once, each on its
+//     own stream and staging: a batch of axis trees or codewords is a latency-bound launch on a few CUs, so batches
+//     run side by side instead of one after another;
+//   * each caller copies its own input into its batch's page-locked staging and its own output back (the copies run
+//     on the callers' threads in parallel), and the kernels read and write that staging directly (zero-copy);
 //   * requests of one shape run as one launch: the encoder over n codewords (RsJob with cw stride = slot size), the
 //     decoder over n codewords (per-codeword descriptors), and axis_roots_kernel over n trees (one workgroup each,
 //     the tree in LDS: one launch instead of a leaf launch plus a launch per level).
@@ -33,12 +35,6 @@
 
 namespace cda {
 
-#ifndef CDA_AXIS_DMA
-#define CDA_AXIS_DMA 0  // diagnostic A/B: staging moved by DMA through a device buffer instead of zero-copy kernels
-#endif
-
-const char* axis_diag_tag() { return CDA_AXIS_DMA ? "axis_dma" : ""; }
-
 namespace {
 
 enum : int { kEnc = 0, kRoot = 1, kDec = 2 };  // group order in a batch: inputs-only kinds first, in+out (decode) last
@@ -47,10 +43,23 @@ enum : int { kQueued = 0, kCopyIn = 1, kCopied = 2, kResult = 3, kDone = 4 };
 // staging of one batch: at most this many bytes (a larger single request runs alone)
 constexpr size_t kBatchBytes = 64ull << 20;
 constexpr size_t kAlign = 512;
+// batches in flight at once (CDA_AXIS_SLOTS in the test-hooks build, 1..kMaxSlots)
+constexpr int kSlots = 4, kMaxSlots = 8;
 
 size_t up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 
 }  // namespace
+
+// One batch in flight: its page-locked staging (host address and the device's alias of it) and its stream.
+struct AxisSlot {
+  uint8_t* h = nullptr;
+  uint8_t* hd = nullptr;
+  size_t cap = 0;
+  hipStream_t s = nullptr;
+  bool busy = false;
+  size_t copy_left = 0, out_left = 0;
+  std::condition_variable lead_cv;  // the batch's leader waits here for its members' copies
+};
 
 struct AxisReq {
   int kind = kEnc;
@@ -59,7 +68,8 @@ struct AxisReq {
   const uint8_t* in = nullptr;       // enc: k*len data; dec: 2k*len shards; root: n*512 leaves
   uint8_t* out = nullptr;            // enc: k*len parity; dec: the shards (missing ones written)
   const uint8_t* present = nullptr;  // dec: 2k flags
-  size_t off = 0, out_off = 0, st_off = 0;  // batch layout (same offsets in the pinned and the device buffer)
+  size_t off = 0, out_off = 0, st_off = 0;  // offsets in the batch's staging
+  AxisSlot* slot = nullptr;                 // the batch's slot, once taken into one
   int state = kQueued;
   int rc = CDA_OK;
   uint8_t rec[CDA_REC_BYTES];  // root: the root record
@@ -72,13 +82,9 @@ struct AxisReq {
 
 struct AxisQueue {
   std::mutex mu;
-  std::condition_variable lead_cv;  // the leader waits here for the copies of its batch
   std::vector<AxisReq*> pending;
-  bool leader = false;
-  size_t copy_left = 0, out_left = 0;
-  uint8_t* h = nullptr;  // page-locked staging of the batch in flight (host address)
-  uint8_t* hd = nullptr;  // the same memory as the device addresses it (zero-copy kernels)
-  size_t h_cap = 0;
+  AxisSlot slot[kMaxSlots];
+  int nslots = kSlots;
 };
 
 namespace {
@@ -94,11 +100,11 @@ struct Group {
 
 struct Layout {
   std::vector<Group> groups;
-  size_t h2d_end = 0;   // H2D [0, h2d_end): inputs, descriptors, decode codewords
-  size_t d2h_begin = 0;  // D2H [d2h_begin, total): decode codewords, parity, root records and status words
   size_t total = 0;
 };
 
+// Staging layout of a batch: inputs of encodes and roots | descriptors | decode codewords (in place) | parity, root
+// records and status words.
 void plan(std::vector<AxisReq*>& batch, Layout& L) {
   std::map<std::tuple<int, uint32_t, uint32_t, uint64_t>, size_t> idx;
   for (AxisReq* r : batch) {
@@ -124,14 +130,12 @@ void plan(std::vector<AxisReq*>& batch, Layout& L) {
     g.desc0 = cur;
     cur += up(g.kind == kRoot ? 8 * g.reqs.size() : g.reqs.size() * (16 + 2 * (size_t)g.k));
   }
-  L.d2h_begin = cur;
   for (Group& g : L.groups) {  // decode codewords (in and out)
     if (g.kind != kDec) continue;
     g.item_in = up((size_t)2 * g.k * g.len);
     g.in0 = cur;
     for (AxisReq* r : g.reqs) r->off = r->out_off = cur, cur += g.item_in;
   }
-  L.h2d_end = cur;
   for (Group& g : L.groups) {  // parity, root records, status words
     if (g.kind == kEnc) {
       g.item_out = up((size_t)g.k * g.len);
@@ -192,80 +196,88 @@ void copy_out(AxisReq* r, const uint8_t* h) {
 
 int code_of(int lr) { return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE; }
 
-// The batch on the device: one H2D, one launch per group, one D2H, one synchronisation.  A group the kernels do not
-// support (-2) fails alone with CDA_E_UNSUPPORTED; a runtime failure fails the batch with CDA_E_DEVICE.
-int run_device(cda_ctx* c, const Layout& L, uint8_t* h, uint8_t* hd) {
-  Lock l(c);
-  hipStream_t s = c->stream;
-#if CDA_AXIS_DMA
-  // A/B: the batch goes up and comes back by DMA through a device buffer
-  (void)hd;
-  if (int rc = ensure(c, c->ax, L.total)) return rc;
-  uint8_t* D = (uint8_t*)c->ax.p;
-  if (!dev_ok(c, hipMemcpyAsync(D, h, L.h2d_end, hipMemcpyHostToDevice, s), "H2D")) return CDA_E_DEVICE;
-#else
-  // zero-copy: the kernels read the inputs from the page-locked staging over PCIe and write the results back into
-  // it -- a batch's bytes cross the link once each way either way, without two DMA submissions per call
-  uint8_t* D = hd;
-#endif
-  for (const Group& g : L.groups) {
-    const int n = (int)g.reqs.size();
-    int lr = 0;
-    if (g.kind == kEnc) {
-      RsJob j{};
-      j.src = D + g.in0;
-      j.src_cw = (long long)g.item_in;
-      j.src_sh = g.len;
-      j.dst = D + g.out0;
-      j.dst_cw = (long long)g.item_out;
-      j.dst_sh = g.len;
-      j.k = (int)g.k;
-      j.cw_per_blk = n;
-      j.nblk = 1;
-      j.shard_len = (int)g.len;
-      const bool ff8 = 2 * g.k <= 256;
-      ProfScope ps(c, ff8 ? "axis_rs_encode8" : "axis_rs_encode16", s);
-      lr = ff8 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
-    } else if (g.kind == kRoot) {
-      ProfScope ps(c, "axis_roots", s);
-      lr = launch_axis_roots(D + g.in0, (long long)g.item_in, (int)g.n, g.ss,
-                             (const unsigned long long*)(D + g.desc0), n, D + g.out0, (unsigned long long*)(D + g.st0),
-                             s);
-    } else {
-      ProfScope ps(c, "axis_rs_decode", s);
-      const uint8_t* d = D + g.desc0;
-      lr = launch_rs_decode(D, (const long long*)d, (const long long*)(d + 8 * (size_t)n), d + 16 * (size_t)n, n,
-                            (int)g.k, (int)g.len, s);
-    }
-    if (lr == -2) {
-      for (AxisReq* r : g.reqs) r->rc = CDA_E_UNSUPPORTED;
-    } else if (lr) {
-      return code_of(lr);
+// The batch on the device: one launch per group on the slot's stream, reading and writing the page-locked staging
+// itself (zero-copy: a batch's bytes cross the link once each way, with no DMA submissions), then one
+// synchronisation of that stream.  The context lock is held only while launching (profiling events, error text),
+// not while the kernels run, so other slots' batches and the block path proceed meanwhile.  A group the kernels do
+// not support (-2) fails alone with CDA_E_UNSUPPORTED; a runtime failure fails the batch with CDA_E_DEVICE.
+int run_device(cda_ctx* c, const Layout& L, AxisSlot* sl) {
+  (void)hipSetDevice(c->device);
+  hipStream_t s = sl->s;
+  uint8_t* D = sl->hd;
+  int rc = CDA_OK;
+  {
+    Lock l(c);
+    for (const Group& g : L.groups) {
+      const int n = (int)g.reqs.size();
+      int lr = 0;
+      if (g.kind == kEnc) {
+        RsJob j{};
+        j.src = D + g.in0;
+        j.src_cw = (long long)g.item_in;
+        j.src_sh = g.len;
+        j.dst = D + g.out0;
+        j.dst_cw = (long long)g.item_out;
+        j.dst_sh = g.len;
+        j.k = (int)g.k;
+        j.cw_per_blk = n;
+        j.nblk = 1;
+        j.shard_len = (int)g.len;
+        const bool ff8 = 2 * g.k <= 256;
+        ProfScope ps(c, ff8 ? "axis_rs_encode8" : "axis_rs_encode16", s);
+        lr = ff8 ? launch_rs_encode8(j, s) : launch_rs_encode16(j, s);
+      } else if (g.kind == kRoot) {
+        ProfScope ps(c, "axis_roots", s);
+        lr = launch_axis_roots(D + g.in0, (long long)g.item_in, (int)g.n, g.ss,
+                               (const unsigned long long*)(D + g.desc0), n, D + g.out0,
+                               (unsigned long long*)(D + g.st0), s);
+      } else {
+        ProfScope ps(c, "axis_rs_decode", s);
+        const uint8_t* d = D + g.desc0;
+        lr = launch_rs_decode(D, (const long long*)d, (const long long*)(d + 8 * (size_t)n), d + 16 * (size_t)n, n,
+                              (int)g.k, (int)g.len, s);
+      }
+      if (lr == -2) {
+        for (AxisReq* r : g.reqs) r->rc = CDA_E_UNSUPPORTED;
+      } else if (lr) {
+        c->last_err = std::string("axis launch: ") + hipGetErrorString(hipGetLastError());
+        rc = code_of(lr);
+        break;
+      }
     }
   }
-#if CDA_AXIS_DMA
-  if (!dev_ok(c, hipMemcpyAsync(h + L.d2h_begin, D + L.d2h_begin, L.total - L.d2h_begin, hipMemcpyDeviceToHost, s),
-              "D2H"))
-    return CDA_E_DEVICE;
-#endif
-  if (!dev_ok(c, hipStreamSynchronize(s), "sync")) return CDA_E_DEVICE;
-  flush_profile(c);
-  return CDA_OK;
+  // always drained, also after a failed launch: earlier launches of the batch may still read the staging
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess || c->prof) {
+    Lock l(c);
+    if (e != hipSuccess) {
+      dev_ok(c, e, "sync");
+      rc = CDA_E_DEVICE;
+    }
+    flush_profile(c);
+  }
+  return rc;
 }
 
-void free_host(AxisQueue* q) {
-  if (!q->h) return;
-  (void)hipHostUnregister(q->h);
-  free(q->h);
-  q->h = q->hd = nullptr;
-  q->h_cap = 0;
+void free_host(AxisSlot* sl) {
+  if (!sl->h) return;
+  (void)hipHostUnregister(sl->h);
+  free(sl->h);
+  sl->h = sl->hd = nullptr;
+  sl->cap = 0;
 }
 
-bool ensure_host(cda_ctx* c, AxisQueue* q, size_t bytes) {
-  if (q->h_cap >= bytes) return true;
-  const size_t cap = (std::max({bytes, (size_t)4 << 20, std::min(2 * q->h_cap, kBatchBytes)}) + 4095) & ~(size_t)4095;
-  free_host(q);
+// The slot's stream (created on first use) and at least `bytes` of staging.
+bool ensure_slot(cda_ctx* c, AxisSlot* sl, size_t bytes) {
   (void)hipSetDevice(c->device);
+  if (!sl->s && hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess) {
+    sl->s = nullptr;
+    (void)hipGetLastError();
+    return false;
+  }
+  if (sl->cap >= bytes) return true;
+  const size_t cap = (std::max({bytes, (size_t)4 << 20, std::min(2 * sl->cap, kBatchBytes)}) + 4095) & ~(size_t)4095;
+  free_host(sl);
   void* p = nullptr;
   void* d = nullptr;
   // page-aligned host memory page-locked by registration (coarse-grained): coherent at the points this queue uses it
@@ -284,22 +296,27 @@ bool ensure_host(cda_ctx* c, AxisQueue* q, size_t bytes) {
     (void)hipGetLastError();
     return false;
   }
-  q->h = (uint8_t*)p;
-  q->hd = (uint8_t*)d;
-  q->h_cap = cap;
+  sl->h = (uint8_t*)p;
+  sl->hd = (uint8_t*)d;
+  sl->cap = cap;
   return true;
 }
 
-// The batch is over: the owner of the oldest queued request (if any) becomes the next leader.
+AxisSlot* free_slot(AxisQueue* q) {
+  for (int i = 0; i < q->nslots; i++)
+    if (!q->slot[i].busy) return &q->slot[i];
+  return nullptr;
+}
+
+// A slot is free again (or a leader gave up): the owner of the oldest queued request, if any, leads the next batch.
 void hand_over(AxisQueue* q) {
-  q->leader = false;
   if (!q->pending.empty()) q->pending.front()->cv.notify_one();
 }
 
-// Runs one batch as its leader: `self` (queued, in q->pending) and whatever else is queued.  lk is held on entry and
-// on return.  Every request of the batch is kDone when it returns, and the staging is free again.
-void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* self) {
-  q->leader = true;
+// Runs one batch as its leader on slot `sl`: `self` (queued, in q->pending) and whatever else is queued.  lk is held
+// on entry and on return.  Every request of the batch is kDone when it returns, and the slot is free again.
+void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* self, AxisSlot* sl) {
+  sl->busy = true;
   std::vector<AxisReq*> batch, rest;
   Layout L;
   int fail = CDA_OK;
@@ -316,7 +333,7 @@ void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* s
       }
     }
     plan(batch, L);
-    if (!ensure_host(c, q, L.total)) fail = CDA_E_NOMEM;
+    if (!ensure_slot(c, sl, L.total)) fail = CDA_E_NOMEM;
   } catch (...) {
     fail = CDA_E_NOMEM;
   }
@@ -324,52 +341,59 @@ void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* s
     q->pending.erase(std::remove(q->pending.begin(), q->pending.end(), self), q->pending.end());
     self->rc = fail;
     self->state = kDone;
+    sl->busy = false;
     hand_over(q);
     return;
   }
   q->pending.swap(rest);
-  q->copy_left = batch.size();
+  sl->copy_left = batch.size();
   for (AxisReq* r : batch) {
+    r->slot = sl;
     r->state = kCopyIn;
     if (r != self) r->cv.notify_one();
   }
+  if (!q->pending.empty() && free_slot(q)) hand_over(q);  // requests this batch could not take may lead another
   lk.unlock();
-  fill_desc(L, q->h);
-  copy_in(self, q->h);
+  fill_desc(L, sl->h);
+  copy_in(self, sl->h);
   lk.lock();
   self->state = kCopied;
-  q->copy_left--;
-  while (q->copy_left > 0) q->lead_cv.wait(lk);
+  sl->copy_left--;
+  while (sl->copy_left > 0) sl->lead_cv.wait(lk);
   lk.unlock();
   int rc;
   try {
-    rc = run_device(c, L, q->h, q->hd);
+    rc = run_device(c, L, sl);
   } catch (...) {
     rc = api_exception(c);
   }
   lk.lock();
-  q->out_left = batch.size();
+  sl->out_left = batch.size();
   for (AxisReq* r : batch) {
     if (r->rc == CDA_OK) r->rc = rc;
     r->state = kResult;
     if (r != self) r->cv.notify_one();
   }
   lk.unlock();
-  if (self->rc == CDA_OK) copy_out(self, q->h);
+  if (self->rc == CDA_OK) copy_out(self, sl->h);
   lk.lock();
   self->state = kDone;
-  q->out_left--;
-  while (q->out_left > 0) q->lead_cv.wait(lk);
+  sl->out_left--;
+  while (sl->out_left > 0) sl->lead_cv.wait(lk);
+  sl->busy = false;
   hand_over(q);
 }
 
 AxisQueue* queue_of(cda_ctx* c) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
-  if (!c->axq) c->axq = new AxisQueue();
+  if (!c->axq) {
+    c->axq = new AxisQueue();
+    if (const char* e = CDA_AB_ENV("CDA_AXIS_SLOTS")) c->axq->nslots = std::max(1, std::min(kMaxSlots, atoi(e)));
+  }
   return c->axq;
 }
 
-// Queues r and returns its rc once its batch has run (this thread may run that batch, or the next one, as leader).
+// Queues r and returns its rc once its batch has run (this thread may lead that batch itself).
 int submit(cda_ctx* c, AxisReq* r) {
   AxisQueue* q = queue_of(c);
   std::unique_lock<std::mutex> lk(q->mu);
@@ -377,24 +401,28 @@ int submit(cda_ctx* c, AxisReq* r) {
   for (;;) {
     if (r->state == kDone) return r->rc;
     if (r->state == kCopyIn) {
+      AxisSlot* sl = r->slot;
       lk.unlock();
-      copy_in(r, q->h);
+      copy_in(r, sl->h);
       lk.lock();
       r->state = kCopied;
-      if (--q->copy_left == 0) q->lead_cv.notify_one();
+      if (--sl->copy_left == 0) sl->lead_cv.notify_one();
       continue;
     }
     if (r->state == kResult) {
+      AxisSlot* sl = r->slot;
       lk.unlock();
-      if (r->rc == CDA_OK) copy_out(r, q->h);
+      if (r->rc == CDA_OK) copy_out(r, sl->h);
       lk.lock();
       r->state = kDone;
-      if (--q->out_left == 0) q->lead_cv.notify_one();
+      if (--sl->out_left == 0) sl->lead_cv.notify_one();
       return r->rc;
     }
-    if (r->state == kQueued && !q->leader) {
-      lead(c, q, lk, r);
-      continue;
+    if (r->state == kQueued) {
+      if (AxisSlot* sl = free_slot(q)) {
+        lead(c, q, lk, r, sl);
+        continue;
+      }
     }
     r->cv.wait(lk);
   }
@@ -443,7 +471,13 @@ int axis_root_wide(cda_ctx* c, uint64_t square_size, uint64_t axis_index, uint32
 
 void free_axisq(cda_ctx* c) {
   if (!c->axq) return;
-  free_host(c->axq);
+  for (AxisSlot& sl : c->axq->slot) {
+    if (sl.s) {
+      (void)hipStreamSynchronize(sl.s);
+      (void)hipStreamDestroy(sl.s);
+    }
+    free_host(&sl);
+  }
   delete c->axq;
   c->axq = nullptr;
 }

@@ -84,9 +84,8 @@ struct cda_ctx {
   // the library does not own -- under cgo, Go heap.  Opt in per context with cda_set_option(CDA_OPT_HUGE_PAGES, 1) or
   // CDA_HUGE_PAGES=1 at cda_init.  A caller that recycles pinned buffers (go/cda's EDS pool) never takes this path.
   bool huge_pages = false;
-  // the per-axis seams (axisq.cpp): queue of concurrent Encode / Decode / Root calls, its device buffer
+  // the per-axis seams (axisq.cpp): queue of concurrent Encode / Decode / Root calls, its batch slots
   cda::AxisQueue* axq = nullptr;
-  Buf ax;
   // profiling
   bool prof = false;
   struct Pending {
@@ -149,8 +148,7 @@ bool consensus_eligible(const cda_ctx* c, uint32_t k);
 int extend_one_host(cda_ctx* c, uint32_t k, const uint8_t* ods, uint8_t* eds_or_null, uint8_t* row_roots,
                     uint8_t* col_roots, uint8_t* dah, cda_err_info* err, size_t ods_pitch = 0);
 void free_consensus(cda_ctx* c);
-void free_axisq(cda_ctx* c);  // axisq.cpp: the per-axis queue's staging
-const char* axis_diag_tag();  // axisq.cpp: "axis_dma" in the DMA A/B build
+void free_axisq(cda_ctx* c);  // axisq.cpp: the per-axis queue's staging and streams
 // RS jobs of the block path: rows (ODS row r -> Q0 copy + Q1 row r) and columns (top half -> bottom half)
 RsJob rows_job(uint32_t k, uint32_t nblocks, const uint8_t* d_ods, uint8_t* d_eds);
 RsJob cols_job(uint32_t k, uint32_t nblocks, uint8_t* d_eds);

@@ -376,7 +376,6 @@ void cda_free(cda_ctx* c) {
       if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     free_consensus(c);  // joins its copy threads first
     free_axisq(c);
-    if (c->ax.p) (void)hipFree(c->ax.p);
     free_pipeline(c);
     free_staging(c);
     if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
@@ -417,7 +416,7 @@ const char* cda_last_device_error(cda_ctx* c) { return c ? c->last_err.c_str() :
 const char* cda_build_info(void) {
   static const std::string info = [] {
     std::string d;
-    for (const char* t : {rs8_diag_tag(), rs16_diag_tag(), axis_diag_tag(), CDA_TEST_HOOKS ? "test_hooks" : ""})
+    for (const char* t : {rs8_diag_tag(), rs16_diag_tag(), CDA_TEST_HOOKS ? "test_hooks" : ""})
       if (*t) d += (d.empty() ? "" : ",") + std::string(t);
     // a release library reads only the deployment options named here (cda_internal.h CDA_AB_ENV)
     return d.empty() ? std::string("release gfx950; env: CDA_NUMA_BIND, CDA_COPY_THREADS") : "diagnostic gfx950 " + d;

@@ -21,6 +21,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <set>
 
 #include "cda_internal.h"
 #include "nmt_dev.h"
@@ -1076,25 +1078,41 @@ __global__ void __launch_bounds__(PIPE ? 512 : 256) axis_roots_kernel(const uint
   if (threadIdx.x == 0) status[t] = bad == 0xFFFFFFFFu ? ~0ull : (unsigned long long)bad;
 }
 
+// The dynamic-LDS limits of both forms, raised once per device to the most any launch asks for: the axis queue
+// launches from several threads at once (csrc/axisq.cpp), and a per-launch limit set by one thread could otherwise
+// lower the limit another thread's larger launch relies on.
+static int axis_roots_limits() {
+  static std::mutex mu;
+  static std::set<int> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count(dev)) return 0;
+  const size_t pipe = (size_t)2 * kAxisRootsPipeLeaves * kKwStride * 4;
+  const size_t wide = std::max((size_t)kAxisRootsMaxLeaves * CDA_REC_BYTES + (size_t)2 * 64 * kKwStride * 4,
+                               (size_t)kAxisRootsKw128MaxLeaves * CDA_REC_BYTES + (size_t)2 * 128 * kKwStride * 4);
+  if (hipFuncSetAttribute((const void*)axis_roots_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)pipe) != hipSuccess ||
+      hipFuncSetAttribute((const void*)axis_roots_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)wide) != hipSuccess)
+    return -1;
+  done.insert(dev);
+  return 0;
+}
+
 int launch_axis_roots(const uint8_t* d_leaves, long long tree_stride, int n, uint64_t square_size,
                       const unsigned long long* d_axis_idx, int ntrees, void* d_roots, unsigned long long* d_status,
                       hipStream_t s) {
   if (ntrees <= 0) return 0;
   if (n < 1 || n > kAxisRootsMaxLeaves) return -2;
+  if (axis_roots_limits()) return -1;
   if (n <= kAxisRootsPipeLeaves) {  // the schedule buffers hold the levels' rows and the records (B) as well
     const size_t lds = (size_t)2 * kAxisRootsPipeLeaves * kKwStride * 4;
-    if (hipFuncSetAttribute((const void*)axis_roots_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return -1;
     hipLaunchKernelGGL(axis_roots_kernel<true>, dim3(ntrees), dim3(512), lds, s, d_leaves, tree_stride, n,
                        (unsigned long long)square_size, d_axis_idx, (uint4*)d_roots, d_status);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   const size_t lds = (size_t)n * CDA_REC_BYTES + (size_t)2 * (n <= kAxisRootsKw128MaxLeaves ? 128 : 64) * kKwStride * 4;
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute((const void*)axis_roots_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
-    return -1;
   hipLaunchKernelGGL(axis_roots_kernel<false>, dim3(ntrees), dim3(256), lds, s, d_leaves, tree_stride, n,
                      (unsigned long long)square_size, d_axis_idx, (uint4*)d_roots, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
