@@ -8,9 +8,9 @@
 // to the device on its own paid a pageable H2D, one or more launches, a pageable D2H and a synchronisation, and
 // concurrent calls queued behind the context mutex one round trip at a time.  Here every call is a request on the
 // context's axis queue (group commit):
-//   * a caller that finds a free batch slot becomes a leader and takes every request queued so far (up to
-//     kBatchBytes of staging); requests that arrive while every slot is busy form the next batch, so a lone caller
-//     pays no wait and concurrent callers share launches.  Up to kSlots batches are in flight at once, each on its
+//   * a caller that finds a free batch slot becomes a leader and takes every request queued so far (up to the
+//     slot's share of kBatchBytes of staging); requests that arrive while every slot is busy form the next batch, so
+//     a lone caller pays no wait and concurrent callers share launches.  Up to kSlots batches are in flight at once, each on its
 //     own stream and staging: a batch of axis trees or codewords is a latency-bound launch on a few CUs, so batches
 //     run side by side instead of one after another;
 //   * each caller copies its own input into its batch's page-locked staging and its own output back (the copies run
@@ -38,9 +38,11 @@ namespace cda {
 namespace {
 
 enum : int { kEnc = 0, kRoot = 1, kDec = 2 };  // group order in a batch: inputs-only kinds first, in+out (decode) last
-enum : int { kQueued = 0, kCopyIn = 1, kCopied = 2, kResult = 3, kDone = 4 };
+// kTaken: in a batch whose leader is still preparing its slot (its owner waits)
+enum : int { kQueued = 0, kTaken = 1, kCopyIn = 2, kCopied = 3, kResult = 4, kDone = 5 };
 
-// staging of one batch: at most this many bytes (a larger single request runs alone)
+// staging of all batches in flight: at most this many bytes, split evenly over the slots (a larger single request
+// runs alone)
 constexpr size_t kBatchBytes = 64ull << 20;
 constexpr size_t kAlign = 512;
 // batches in flight at once (CDA_AXIS_SLOTS in the test-hooks build, 1..kMaxSlots)
@@ -85,6 +87,8 @@ struct AxisQueue {
   std::vector<AxisReq*> pending;
   AxisSlot slot[kMaxSlots];
   int nslots = kSlots;
+  size_t batch_bytes = kBatchBytes / kSlots;  // staging per slot (kBatchBytes / nslots)
+  size_t largest = 0;  // the largest staging any slot has needed: a slot that grows grows to at least this
 };
 
 namespace {
@@ -267,8 +271,8 @@ void free_host(AxisSlot* sl) {
   sl->cap = 0;
 }
 
-// The slot's stream (created on first use) and at least `bytes` of staging.
-bool ensure_slot(cda_ctx* c, AxisSlot* sl, size_t bytes) {
+// The slot's stream (created on first use) and at least `bytes` of staging (`hint`: the size to grow to at least).
+bool ensure_slot(cda_ctx* c, AxisSlot* sl, size_t bytes, size_t hint, size_t limit) {
   (void)hipSetDevice(c->device);
   if (!sl->s && hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess) {
     sl->s = nullptr;
@@ -276,7 +280,8 @@ bool ensure_slot(cda_ctx* c, AxisSlot* sl, size_t bytes) {
     return false;
   }
   if (sl->cap >= bytes) return true;
-  const size_t cap = (std::max({bytes, (size_t)4 << 20, std::min(2 * sl->cap, kBatchBytes)}) + 4095) & ~(size_t)4095;
+  const size_t cap =
+      (std::max({bytes, hint, std::min((size_t)4 << 20, limit), std::min(2 * sl->cap, limit)}) + 4095) & ~(size_t)4095;
   free_host(sl);
   void* p = nullptr;
   void* d = nullptr;
@@ -325,7 +330,7 @@ void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* s
     rest.reserve(q->pending.size());
     size_t bytes = 0;
     for (AxisReq* r : q->pending) {
-      if (batch.empty() || bytes + r->bytes() <= kBatchBytes || r == self) {
+      if (batch.empty() || bytes + r->bytes() <= q->batch_bytes || r == self) {
         batch.push_back(r);
         bytes += r->bytes();
       } else {
@@ -333,11 +338,33 @@ void lead(cda_ctx* c, AxisQueue* q, std::unique_lock<std::mutex>& lk, AxisReq* s
       }
     }
     plan(batch, L);
-    if (!ensure_slot(c, sl, L.total)) fail = CDA_E_NOMEM;
   } catch (...) {
     fail = CDA_E_NOMEM;
   }
-  if (fail) {  // only this caller's request fails; the others stay queued for the next leader
+  if (!fail && (!sl->s || sl->cap < L.total)) {
+    // The slot's stream or staging is set up without the queue lock (registering tens of MiB takes milliseconds,
+    // and every other caller needs the lock to move on); the batch's requests leave the queue meanwhile (kTaken).
+    q->pending.swap(rest);
+    for (AxisReq* r : batch) r->state = kTaken;
+    q->largest = std::max(q->largest, L.total);
+    const size_t hint = std::min(q->largest, q->batch_bytes);
+    lk.unlock();
+    bool ok = false;
+    try {
+      ok = ensure_slot(c, sl, L.total, hint, q->batch_bytes);
+    } catch (...) {
+    }
+    lk.lock();
+    if (!ok) {  // only this caller's request fails; the others go back to the head of the queue, in order
+      fail = CDA_E_NOMEM;
+      std::vector<AxisReq*> back;
+      for (AxisReq* r : batch)
+        if (r != self) r->state = kQueued, back.push_back(r);
+      q->pending.insert(q->pending.begin(), back.begin(), back.end());
+    }
+    rest = q->pending;  // requests queued meanwhile stay queued
+  }
+  if (fail) {
     q->pending.erase(std::remove(q->pending.begin(), q->pending.end(), self), q->pending.end());
     self->rc = fail;
     self->state = kDone;
@@ -389,6 +416,7 @@ AxisQueue* queue_of(cda_ctx* c) {
   if (!c->axq) {
     c->axq = new AxisQueue();
     if (const char* e = CDA_AB_ENV("CDA_AXIS_SLOTS")) c->axq->nslots = std::max(1, std::min(kMaxSlots, atoi(e)));
+    c->axq->batch_bytes = kBatchBytes / c->axq->nslots;
   }
   return c->axq;
 }
