@@ -35,6 +35,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -494,12 +495,21 @@ static void mode_extend(int k, int threads, int reps, const uint8_t* ods, const 
     memset(s.eds, 0, (size_t)w * w * SHARE);
     for (int r = 0; r < k; r++) memcpy(cell(&s, r, 0), ods + (size_t)r * k * SHARE, (size_t)k * SHARE);
     atomic_store(&P.rc, 0);
+    struct rusage u0, u1;
+    getrusage(RUSAGE_SELF, &u0);
     const double a = now_s();
     pool_run(t_phase1, &s, k);
     pool_run(t_phase2, &s, k);
     const double b = now_s();
     pool_run(t_roots, &s, w);
     const double c = now_s();
+    getrusage(RUSAGE_SELF, &u1);
+    if (getenv("RSMT2D_AXES_VERBOSE")) /* per-rep phases and the process's CPU time over the rep (diagnosis) */
+      fprintf(stderr, "rep %d extend %.3f roots %.3f ms cpu user %.1f sys %.1f ms ctxsw %ld/%ld\n", it, 1e3 * (b - a),
+              1e3 * (c - b),
+              1e3 * (u1.ru_utime.tv_sec - u0.ru_utime.tv_sec) + 1e-3 * (u1.ru_utime.tv_usec - u0.ru_utime.tv_usec),
+              1e3 * (u1.ru_stime.tv_sec - u0.ru_stime.tv_sec) + 1e-3 * (u1.ru_stime.tv_usec - u0.ru_stime.tv_usec),
+              u1.ru_nvcsw - u0.ru_nvcsw, u1.ru_nivcsw - u0.ru_nivcsw);
     if (atomic_load(&P.rc)) {
       fprintf(stderr, "call failed rc=%d\n", atomic_load(&P.rc));
       exit(3);
