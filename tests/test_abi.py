@@ -126,7 +126,7 @@ def test_release_library_reads_no_environment_per_call():
 # The A/B switches of the measured experiments: test / diagnostic builds only.
 AB_KNOBS = ("CDA_CONSENSUS", "CDA_CONS_IN", "CDA_CONS_OUT", "CDA_CONS_STG", "CDA_CONS_TRACE", "CDA_RS16",
             "CDA_RS16_LDS_KB", "CDA_RS8_LAT_U", "CDA_REPAIR_OVERLAP", "CDA_REPAIR_FUSED", "CDA_REPAIR_EARLY",
-            "CDA_REPAIR_TRACE", "CDA_STAGING", "CDA_TREES_LDS", "CDA_HUGE_PAGES", "CDA_FAULT_INJECT")
+            "CDA_REPAIR_TRACE", "CDA_STAGING", "CDA_TREES_LDS", "CDA_HUGE_PAGES", "CDA_FAULT_INJECT", "CDA_AXIS_SLOTS")
 
 
 def test_release_library_ignores_ab_knobs():
