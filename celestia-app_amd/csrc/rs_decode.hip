@@ -100,11 +100,10 @@ __device__ __forceinline__ void mul_lane(uint32_t (&X)[PL], const uint32_t (&Y)[
   muladd_lane<PL>(X, Y, c);
 }
 
-// raw bytes (unit) <-> planes
+// raw bytes (unit, already loaded as PL / 4 16-byte words) -> planes
 template <int PL>
-__device__ __forceinline__ void load_unit(const uint8_t* p, uint32_t (&v)[PL]) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
-  if (PL == 8) {
+__device__ __forceinline__ void planes_of_raw(const uint4 (&q)[PL / 4], uint32_t (&v)[PL]) {
+  if constexpr (PL == 8) {
     const uint4 a = q[0], b = q[1];
     uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     bitslice8(w);
@@ -124,6 +123,8 @@ __device__ __forceinline__ void load_unit(const uint8_t* p, uint32_t (&v)[PL]) {
   }
   apply<PL>(v, Field<PL>::phi);
 }
+
+// planes -> raw bytes (unit)
 template <int PL>
 __device__ __forceinline__ void store_unit(uint8_t* p, uint32_t (&v)[PL]) {
   apply<PL>(v, Field<PL>::phi_inv);
@@ -291,30 +292,61 @@ __global__ void __launch_bounds__(256) rs_decode_kernel(DecArgs a) {
   const int ne = ecount;
   for (int p = threadIdx.x; p < a.m + a.k; p += blockDim.x) {
     unsigned acc = 0;  // ne < 2^11 terms below 2^16: no overflow
-    for (int t = 0; t < ne; t++) {
+    int t = 0;
+    // eight erasures per step: their indices and log entries are independent LDS reads issued together, not a chain
+    // of dependent round trips (the sum was ~128 serial elist -> ltab pairs per thread at 50 % loss)
+    for (; t + 8 <= ne; t += 8) {
+      int j[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) j[u] = elist[t + u];
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc += j[u] != p ? ltab[p ^ j[u]] : 0u;
+    }
+    for (; t < ne; t++) {
       const int j = elist[t];
       acc += j != p ? ltab[p ^ j] : 0u;
     }
     errl[p] = (uint16_t)(acc % Field<PL>::kMod);
   }
   __syncthreads();
-  // work[p] = shard(p) * exp(errLocs[p]) (present), else 0
-  for (int e = threadIdx.x; e < (a.n << a.log2U); e += blockDim.x) {
-    const int p = e >> a.log2U, u = e & (U - 1);
-    int shard = -1;
-    if (p < a.k) shard = pres[a.k + p] ? a.k + p : -1;
-    else if (p >= a.m && p < a.m + a.k) shard = pres[p - a.m] ? p - a.m : -1;
-    uint32_t v[PL];
-    if (shard >= 0) {
-      uint32_t raw[PL];
-      load_unit<PL>(base + shard * sstride + u * (PL * 4), raw);
-      mul_lane<PL>(v, raw, cpoly_of_log<PL>(a, errl[p]));
-    } else {
+  // work[p] = shard(p) * exp(errLocs[p]) (present), else 0.  A thread owns at most 4 items (n * U <= 1024 at the
+  // launch); all of its loads are issued before the first is used, so the phase waits on memory once.
+  {
+    const int items = a.n << a.log2U;
+    uint4 raw[4][PL / 4];
+    int shard[4];
 #pragma unroll
-      for (int j = 0; j < PL; j++) v[j] = 0;
+    for (int it = 0; it < 4; it++) {
+      const int e = threadIdx.x + it * blockDim.x;
+      shard[it] = -1;
+      if (e < items) {
+        const int p = e >> a.log2U, u = e & (U - 1);
+        if (p < a.k) shard[it] = pres[a.k + p] ? a.k + p : -1;
+        else if (p >= a.m && p < a.m + a.k) shard[it] = pres[p - a.m] ? p - a.m : -1;
+        if (shard[it] >= 0) {
+          const uint4* q = reinterpret_cast<const uint4*>(base + shard[it] * sstride + u * (PL * 4));
+#pragma unroll
+          for (int h = 0; h < PL / 4; h++) raw[it][h] = q[h];
+        }
+      }
     }
 #pragma unroll
-    for (int j = 0; j < PL; j++) st[j * nU + p * U + u] = v[j];
+    for (int it = 0; it < 4; it++) {
+      const int e = threadIdx.x + it * blockDim.x;
+      if (e >= items) continue;
+      const int p = e >> a.log2U, u = e & (U - 1);
+      uint32_t v[PL];
+      if (shard[it] >= 0) {
+        uint32_t w[PL];
+        planes_of_raw<PL>(raw[it], w);
+        mul_lane<PL>(v, w, cpoly_of_log<PL>(a, errl[p]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < PL; j++) v[j] = 0;
+      }
+#pragma unroll
+      for (int j = 0; j < PL; j++) st[j * nU + p * U + u] = v[j];
+    }
   }
   __syncthreads();
   {  // IFFT: layers D = 1, 2, 4, ... (GF(2^8): two per LDS round trip; GF(2^16) keeps one, its quad
@@ -466,6 +498,10 @@ int launch_rs_decode(uint8_t* d_base, const long long* d_off, const long long* d
   int U = 16;
   while (U > 1 && (units % U || a.n * U > 1024)) U >>= 1;  // <= 4 derivative items per thread
   if (a.n * U > 1024) return -2;                          // n > 1024 (k > 512): not on the device path yet
+  // A few codewords (the per-axis Decode, a short crossword batch) leave most CUs idle: split each codeword's bytes
+  // over more workgroups (fewer units each) until the launch has 512 of them -- a workgroup's latency falls with its
+  // items per thread, and the error locator it recomputes is cheap next to that.
+  while (U > 1 && (long long)ncw * (units / U) < 512) U >>= 1;
   a.U = U;
   a.log2U = dec::ilog2(U);
   a.slices = units / U;
