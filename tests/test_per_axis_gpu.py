@@ -96,6 +96,36 @@ def test_concurrent_mixed_shapes_match_oracle(ctx):
                 assert np.array_equal(got, want), f"job {j} ({kind}) rep {rep}"
 
 
+def test_oversized_requests_beside_small_ones(ctx):
+    """Requests larger than one batch slot's share of the staging (csrc/axisq.cpp: 64 MiB over 4 slots) run alone in
+    a slot grown to fit them, while small requests keep flowing through the other slots; every result is the
+    oracle's."""
+    rng = np.random.default_rng(23)
+    big = [rng.integers(0, 256, (32, 512 * 1024), dtype=np.uint8) for _ in range(2)]  # 16 MiB in + 16 MiB out each
+    big_want = [O.leo_encode(d) for d in big]
+    small = [rng.integers(0, 256, (16, 512), dtype=np.uint8) for _ in range(24)]
+    small_want = [O.leo_encode(d) for d in small]
+    got_big, got_small = [None] * len(big), [[None] * 8 for _ in small]
+
+    def run_big(i):
+        def f():
+            got_big[i] = ctx.rs_encode(big[i])
+        return f
+
+    def run_small(i):
+        def f():
+            for rep in range(8):
+                got_small[i][rep] = ctx.rs_encode(small[i])
+        return f
+
+    _run_threads([run_big(i) for i in range(len(big))] + [run_small(i) for i in range(len(small))])
+    for i in range(len(big)):
+        assert np.array_equal(got_big[i], big_want[i]), f"big {i}"
+    for i in range(len(small)):
+        for rep in range(8):
+            assert np.array_equal(got_small[i][rep], small_want[i]), f"small {i} rep {rep}"
+
+
 def test_axis_root_edge_cases_match_oracle(ctx):
     """Tree shapes the wrapper allows: one leaf, odd and ragged counts, a push-order violation (the reference's error
     with the offending leaf), and a tree wider than one workgroup's LDS (the generic level path)."""
