@@ -10,9 +10,9 @@
 // context's axis queue (group commit):
 //   * a caller that finds a free batch slot becomes a leader and takes every request queued so far (up to the
 //     slot's share of kBatchBytes of staging); requests that arrive while every slot is busy form the next batch, so
-//     a lone caller pays no wait and concurrent callers share launches.  Up to kSlots batches are in flight at once, each on its
-//     own stream and staging: a batch of axis trees or codewords is a latency-bound launch on a few CUs, so batches
-//     run side by side instead of one after another;
+//     a lone caller pays no wait and concurrent callers share launches.  Up to kSlots batches are in flight at once,
+//     each on its own stream and staging: a batch of axis trees or codewords is a latency-bound launch on a few CUs,
+//     so batches run side by side instead of one after another;
 //   * each caller copies its own input into its batch's page-locked staging and its own output back (the copies run
 //     on the callers' threads in parallel), and the kernels read and write that staging directly (zero-copy);
 //   * requests of one shape run as one launch: the encoder over n codewords (RsJob with cw stride = slot size), the
