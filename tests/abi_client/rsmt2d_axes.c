@@ -598,9 +598,15 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (use_cda) p_cda_free(g_ctx);
-  /* leave without the exit-time destructors of the HIP runtime (under the host-ASan build the ASan runtime's own
-     checks fire inside them, after every libcda call has returned; tests/abi_client/abi_host_client.c does the same) */
+  /* The host-ASan build leaves without the exit-time destructors of the HIP runtime (the ASan runtime's own checks
+     fire inside them, after every libcda call has returned; tests/abi_client/abi_host_client.c does the same).  The
+     plain build exits normally, so that a profiler's exit-time output (rocprofv3) is written. */
   fflush(stdout);
   fflush(stderr);
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
   _exit(0);
+#endif
+#endif
+  return 0;
 }
