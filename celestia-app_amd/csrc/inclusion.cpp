@@ -175,12 +175,16 @@ int cda_merkle_roots(cda_ctx* c, uint32_t nsets, const uint32_t* set_offsets, co
   CDA_API_CATCH(c)
 }
 
-int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares, uint8_t* eds_or_null,
-                            uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, uint8_t* row_nodes,
-                            uint8_t* col_nodes, uint8_t* dah_nodes, cda_err_info* err) {
-  CDA_API_TRY
-  set_err(err, CDA_OK, -1, -1, -1, -1);
-  if (!c || !shares || !row_roots || !col_roots || !dah) return CDA_E_ARG;
+}  // extern "C"
+
+namespace {
+
+// cda_extend_commit_nodes with the row trees' nodes exported for rows [row_lo, row_hi) only (row_nodes then holds
+// row_hi - row_lo trees): a share proof needs the trees of its own rows, not all 2k of them.
+int extend_commit_nodes_rows(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares,
+                             uint8_t* eds_or_null, uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah,
+                             uint8_t* row_nodes, uint32_t row_lo, uint32_t row_hi, uint8_t* col_nodes,
+                             uint8_t* dah_nodes, cda_err_info* err) {
   uint32_t k = 0;
   if (int rc = square_k(count, share_len, &k, err)) return rc;
   Lock l(c);
@@ -212,10 +216,17 @@ int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, cons
     if (launch_leaf_hash((const uint8_t*)c->eds.p, c->leaf.p, d_status, (int)k, 1, s)) return CDA_E_DEVICE;
   }
   const bool want = row_nodes || col_nodes;
+  // with column trees, every level is copied whole; rows only: trees row_lo.. of each level (contiguous: the leaves
+  // are cell-major and the levels [tree][n], rows first)
+  const bool whole = col_nodes != nullptr;
+  if (row_hi > w || row_lo >= row_hi) row_lo = 0, row_hi = w;
+  const uint32_t t0 = whole ? 0 : row_lo, nt = whole ? w : row_hi - row_lo;
   std::vector<std::vector<uint8_t>> lv((size_t)L + 1);
   if (want) {  // stream order: each copy completes before a later level overwrites its buffer
-    lv[0].resize(cells * CDA_REC_BYTES);
-    if (!dev_ok(c, hipMemcpyAsync(lv[0].data(), c->leaf.p, lv[0].size(), hipMemcpyDeviceToHost, s), "D2H"))
+    lv[0].resize((whole ? cells : (size_t)nt * w) * CDA_REC_BYTES);
+    if (!dev_ok(c, hipMemcpyAsync(lv[0].data(), (uint8_t*)c->leaf.p + (size_t)t0 * w * CDA_REC_BYTES, lv[0].size(),
+                                  hipMemcpyDeviceToHost, s),
+                "D2H"))
       return CDA_E_DEVICE;
   }
   void* bufs[2] = {c->leaf.p, c->scratch.p};
@@ -226,8 +237,11 @@ int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, cons
       if (launch_nmt_level(bufs[(level - 1) & 1], out, level == 1, (int)k, 1, level, s)) return CDA_E_DEVICE;
     }
     if (want) {
-      lv[level].resize((size_t)2 * w * (w >> level) * CDA_REC_BYTES);
-      if (!dev_ok(c, hipMemcpyAsync(lv[level].data(), out, lv[level].size(), hipMemcpyDeviceToHost, s), "D2H"))
+      const size_t nh = w >> level;
+      lv[level].resize((whole ? (size_t)2 * w : (size_t)nt) * nh * CDA_REC_BYTES);
+      if (!dev_ok(c, hipMemcpyAsync(lv[level].data(), (uint8_t*)out + (size_t)t0 * nh * CDA_REC_BYTES,
+                                    lv[level].size(), hipMemcpyDeviceToHost, s),
+                  "D2H"))
         return CDA_E_DEVICE;
     }
   }
@@ -260,16 +274,17 @@ int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, cons
   for (int axis = 0; axis < 2 && want; axis++) {
     uint8_t* out = axis == 0 ? row_nodes : col_nodes;
     if (!out) continue;
-    for (uint32_t t = 0; t < w; t++) {
-      uint8_t* base = out + (size_t)t * per_tree * CDA_NODE_SIZE;
+    const uint32_t tb = axis == 0 ? row_lo : 0, te = axis == 0 ? row_hi : w;
+    for (uint32_t t = tb; t < te; t++) {
+      uint8_t* base = out + (size_t)(t - tb) * per_tree * CDA_NODE_SIZE;
       for (uint32_t i = 0; i < w; i++) {
-        const size_t cell = axis == 0 ? (size_t)t * w + i : (size_t)i * w + t;
+        const size_t cell = (axis == 0 ? (size_t)t * w + i : (size_t)i * w + t) - (size_t)t0 * w;
         memcpy(base + (size_t)i * CDA_NODE_SIZE, lv[0].data() + cell * CDA_REC_BYTES, CDA_NODE_SIZE);
       }
       size_t o = w;
       for (int h = 1; h <= L; h++) {
         const uint32_t nh = w >> h;
-        const uint8_t* src = lv[h].data() + ((size_t)axis * w + t) * nh * CDA_REC_BYTES;
+        const uint8_t* src = lv[h].data() + ((size_t)axis * w + t - t0) * nh * CDA_REC_BYTES;
         for (uint32_t p = 0; p < nh; p++)
           memcpy(base + (o + p) * CDA_NODE_SIZE, src + (size_t)p * CDA_REC_BYTES, CDA_NODE_SIZE);
         o += nh;
@@ -277,6 +292,20 @@ int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, cons
     }
   }
   return map_status(st, 0, err);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cda_extend_commit_nodes(cda_ctx* c, uint32_t count, uint32_t share_len, const uint8_t* shares, uint8_t* eds_or_null,
+                            uint8_t* row_roots, uint8_t* col_roots, uint8_t* dah, uint8_t* row_nodes,
+                            uint8_t* col_nodes, uint8_t* dah_nodes, cda_err_info* err) {
+  CDA_API_TRY
+  set_err(err, CDA_OK, -1, -1, -1, -1);
+  if (!c || !shares || !row_roots || !col_roots || !dah) return CDA_E_ARG;
+  return extend_commit_nodes_rows(c, count, share_len, shares, eds_or_null, row_roots, col_roots, dah, row_nodes, 0,
+                                  ~0u, col_nodes, dah_nodes, err);
   CDA_API_CATCH(c)
 }
 
@@ -295,13 +324,14 @@ int cda_share_inclusion_proof(cda_ctx* c, uint32_t count, uint32_t share_len, co
   const uint32_t w = 2 * k;
   const int L = ilog2i(w);
   const size_t per_tree = 2 * (size_t)w - 1;
-  std::vector<uint8_t> rr((size_t)w * CDA_NODE_SIZE), cr((size_t)w * CDA_NODE_SIZE),
-      rn((size_t)w * per_tree * CDA_NODE_SIZE), dn((2 * (size_t)(2 * w) - 1) * 32);
-  uint8_t root[32];
-  if (int rc = cda_extend_commit_nodes(c, count, share_len, shares, nullptr, rr.data(), cr.data(), root, rn.data(),
-                                       nullptr, dn.data(), err))
-    return rc;
   const uint32_t start_row = start / k, end_row = (end - 1) / k;
+  // only the proof's own row trees come back (rn: rows start_row..end_row)
+  std::vector<uint8_t> rr((size_t)w * CDA_NODE_SIZE), cr((size_t)w * CDA_NODE_SIZE),
+      rn((size_t)(end_row - start_row + 1) * per_tree * CDA_NODE_SIZE), dn((2 * (size_t)(2 * w) - 1) * 32);
+  uint8_t root[32];
+  if (int rc = extend_commit_nodes_rows(c, count, share_len, shares, nullptr, rr.data(), cr.data(), root, rn.data(),
+                                        start_row, end_row + 1, nullptr, dn.data(), err))
+    return rc;
   info->start_row = start_row;
   info->end_row = end_row;
   info->nrows = end_row - start_row + 1;
@@ -328,7 +358,7 @@ int cda_share_inclusion_proof(cda_ctx* c, uint32_t count, uint32_t share_len, co
     nmt_start[i] = (int32_t)s;
     nmt_end[i] = (int32_t)e;
     nmt_count[i] = (int32_t)nodes.size();
-    const uint8_t* tree = rn.data() + (size_t)r * per_tree * CDA_NODE_SIZE;
+    const uint8_t* tree = rn.data() + (size_t)i * per_tree * CDA_NODE_SIZE;
     for (size_t q = 0; q < nodes.size(); q++)
       memcpy(nmt_nodes + ((size_t)i * info->max_nodes + q) * CDA_NODE_SIZE,
              tree_node(tree, w, nodes[q].first, nodes[q].second), CDA_NODE_SIZE);
