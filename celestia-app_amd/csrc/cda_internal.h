@@ -137,6 +137,9 @@ int launch_blob_mountain_level(const BlobDesc* d_desc, int nblobs, void* d_recs,
 // RFC-6962 root (merkle.HashFromByteSlices) of each set of 90-B node records: set s =
 // records idx[off[s] .. off[s+1]) (idx == null: records off[s] ..).  out: nsets x 32 B.
 // nodes_out (nsets == 1 only): every level's 32-B digests, leaves first.  -2: set too large.
+// node export: level h's 90-byte nodes of trees [t0, t0 + nt) (col: column trees) into per-tree node lists
+int launch_pack_tree_level(const void* d_recs, void* d_out, int log2w, int h, bool col, uint32_t t0, uint32_t nt,
+                           uint32_t off_h, hipStream_t s);
 int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t* d_off, int nsets, int max_set,
                        void* d_out, void* d_nodes_out, hipStream_t s);
 

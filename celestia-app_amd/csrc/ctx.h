@@ -55,6 +55,7 @@ struct cda_ctx {
   };
   Buf ods, eds, leaf, scratch, roots, dah, status, plan, payload;
   Buf done;  // per-block tree counters of the small-batch tree launch (trees_lds_kernel), kept at zero
+  Buf nodes;  // node export (inclusion.cpp): the exported trees' per-tree node lists, packed on the device
   // one square split over devices (split.cpp): this device's slab, row / column slabs, leaf records, send blocks,
   // tree scratch, per-device results (meta) and, on the first device, the gathered results
   Buf sp_ods, sp_R, sp_LR, sp_S, sp_C, sp_LC, sp_scratch, sp_meta, sp_gather;

@@ -365,7 +365,7 @@ void cda_free(cda_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     flush_profile(c);
     for (auto* b : {&c->ods, &c->eds, &c->leaf, &c->scratch, &c->roots, &c->dah, &c->status, &c->plan, &c->payload,
-                    &c->rdesc, &c->rcompact, &c->rruns, &c->done, &c->sp_ods, &c->sp_R, &c->sp_LR, &c->sp_S, &c->sp_C, &c->sp_LC, &c->sp_scratch,
+                    &c->rdesc, &c->rcompact, &c->rruns, &c->done, &c->nodes, &c->sp_ods, &c->sp_R, &c->sp_LR, &c->sp_S, &c->sp_C, &c->sp_LC, &c->sp_scratch,
                     &c->sp_meta, &c->sp_gather})
       if (b->p) (void)hipFree(b->p);
     for (auto e : c->sp_ev)

@@ -215,20 +215,23 @@ int extend_commit_nodes_rows(cda_ctx* c, uint32_t count, uint32_t share_len, con
     ProfScope ps(c, "leaf_hash", s);
     if (launch_leaf_hash((const uint8_t*)c->eds.p, c->leaf.p, d_status, (int)k, 1, s)) return CDA_E_DEVICE;
   }
-  const bool want = row_nodes || col_nodes;
-  // with column trees, every level is copied whole; rows only: trees row_lo.. of each level (contiguous: the leaves
-  // are cell-major and the levels [tree][n], rows first)
-  const bool whole = col_nodes != nullptr;
+  // The exported trees' nodes are packed on the device into the per-tree lists the caller gets (rows [row_lo, row_hi),
+  // every column tree when asked), level by level before the next level overwrites its ping-pong buffer, and come
+  // back in one copy per kind.
   if (row_hi > w || row_lo >= row_hi) row_lo = 0, row_hi = w;
-  const uint32_t t0 = whole ? 0 : row_lo, nt = whole ? w : row_hi - row_lo;
-  std::vector<std::vector<uint8_t>> lv((size_t)L + 1);
-  if (want) {  // stream order: each copy completes before a later level overwrites its buffer
-    lv[0].resize((whole ? cells : (size_t)nt * w) * CDA_REC_BYTES);
-    if (!dev_ok(c, hipMemcpyAsync(lv[0].data(), (uint8_t*)c->leaf.p + (size_t)t0 * w * CDA_REC_BYTES, lv[0].size(),
-                                  hipMemcpyDeviceToHost, s),
-                "D2H"))
-      return CDA_E_DEVICE;
-  }
+  const size_t per_tree = 2 * (size_t)w - 1;
+  const size_t rows_b = row_nodes ? (size_t)(row_hi - row_lo) * per_tree * CDA_NODE_SIZE : 0;
+  const size_t cols_b = col_nodes ? (size_t)w * per_tree * CDA_NODE_SIZE : 0;
+  if (rows_b + cols_b && (rc = ensure(c, c->nodes, rows_b + cols_b))) return rc;
+  uint8_t* d_rn = (uint8_t*)c->nodes.p;
+  uint8_t* d_cn = d_rn + rows_b;
+  auto pack = [&](const void* recs, int h, uint32_t off_h) {
+    return (row_nodes && launch_pack_tree_level(recs, d_rn, L, h, false, row_lo, row_hi - row_lo, off_h, s)) ||
+           (col_nodes && launch_pack_tree_level(recs, d_cn, L, h, true, 0, w, off_h, s));
+  };
+  uint32_t off_h = 0;
+  if (pack(c->leaf.p, 0, off_h)) return CDA_E_DEVICE;
+  off_h += w;
   void* bufs[2] = {c->leaf.p, c->scratch.p};
   for (int level = 1; level <= L; level++) {
     void* out = level == L ? c->roots.p : bufs[level & 1];
@@ -236,14 +239,8 @@ int extend_commit_nodes_rows(cda_ctx* c, uint32_t count, uint32_t share_len, con
       ProfScope ps(c, level == 1 ? "nmt_level1" : "nmt_level", s);
       if (launch_nmt_level(bufs[(level - 1) & 1], out, level == 1, (int)k, 1, level, s)) return CDA_E_DEVICE;
     }
-    if (want) {
-      const size_t nh = w >> level;
-      lv[level].resize((whole ? (size_t)2 * w : (size_t)nt) * nh * CDA_REC_BYTES);
-      if (!dev_ok(c, hipMemcpyAsync(lv[level].data(), (uint8_t*)out + (size_t)t0 * nh * CDA_REC_BYTES,
-                                    lv[level].size(), hipMemcpyDeviceToHost, s),
-                  "D2H"))
-        return CDA_E_DEVICE;
-    }
+    if (pack(out, level, off_h)) return CDA_E_DEVICE;
+    off_h += w >> level;
   }
   {
     ProfScope ps(c, "dah", s);
@@ -261,6 +258,8 @@ int extend_commit_nodes_rows(cda_ctx* c, uint32_t count, uint32_t share_len, con
   std::vector<uint8_t> recs(roots_b);
   uint64_t st = 0;
   if ((eds_or_null && !dev_ok(c, hipMemcpyAsync(eds_or_null, c->eds.p, eds_b, hipMemcpyDeviceToHost, s), "D2H")) ||
+      (rows_b && !dev_ok(c, hipMemcpyAsync(row_nodes, d_rn, rows_b, hipMemcpyDeviceToHost, s), "D2H")) ||
+      (cols_b && !dev_ok(c, hipMemcpyAsync(col_nodes, d_cn, cols_b, hipMemcpyDeviceToHost, s), "D2H")) ||
       !dev_ok(c, hipMemcpyAsync(recs.data(), c->roots.p, roots_b, hipMemcpyDeviceToHost, s), "D2H") ||
       !dev_ok(c, hipMemcpyAsync(dah, d_dah, 32, hipMemcpyDeviceToHost, s), "D2H") ||
       !dev_ok(c, hipMemcpyAsync(&st, d_status, 8, hipMemcpyDeviceToHost, s), "D2H") ||
@@ -269,28 +268,6 @@ int extend_commit_nodes_rows(cda_ctx* c, uint32_t count, uint32_t share_len, con
   flush_profile(c);
   pack_roots(recs.data(), w, row_roots);
   pack_roots(recs.data() + (size_t)w * CDA_REC_BYTES, w, col_roots);
-  // level buffers -> per-tree node lists: leaves (cell-major records), then [tree][n] levels
-  const size_t per_tree = 2 * (size_t)w - 1;
-  for (int axis = 0; axis < 2 && want; axis++) {
-    uint8_t* out = axis == 0 ? row_nodes : col_nodes;
-    if (!out) continue;
-    const uint32_t tb = axis == 0 ? row_lo : 0, te = axis == 0 ? row_hi : w;
-    for (uint32_t t = tb; t < te; t++) {
-      uint8_t* base = out + (size_t)(t - tb) * per_tree * CDA_NODE_SIZE;
-      for (uint32_t i = 0; i < w; i++) {
-        const size_t cell = (axis == 0 ? (size_t)t * w + i : (size_t)i * w + t) - (size_t)t0 * w;
-        memcpy(base + (size_t)i * CDA_NODE_SIZE, lv[0].data() + cell * CDA_REC_BYTES, CDA_NODE_SIZE);
-      }
-      size_t o = w;
-      for (int h = 1; h <= L; h++) {
-        const uint32_t nh = w >> h;
-        const uint8_t* src = lv[h].data() + ((size_t)axis * w + t - t0) * nh * CDA_REC_BYTES;
-        for (uint32_t p = 0; p < nh; p++)
-          memcpy(base + (o + p) * CDA_NODE_SIZE, src + (size_t)p * CDA_REC_BYTES, CDA_NODE_SIZE);
-        o += nh;
-      }
-    }
-  }
   return map_status(st, 0, err);
 }
 

@@ -250,6 +250,36 @@ int launch_blob_mountain_level(const BlobDesc* d_desc, int nblobs, void* d_recs,
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Node export, one level at a time: the 90-byte nodes of level h of trees [t0, t0 + nt) of one kind (rows: trees
+// 0..w-1 of the level buffer, columns: w..2w-1; leaves: the cell-major records) into the per-tree node lists
+// out[t - t0][off_h + p] (2w - 1 nodes of 90 B per tree, leaves first, root last) -- the layout the export hands back,
+// built on the device so that one copy moves it (no host repacking of 96-byte records).  One thread per node, 45
+// two-byte words (a 90-byte node is 2-byte aligned).
+__global__ void __launch_bounds__(256) pack_tree_level_kernel(const uint8_t* __restrict__ recs, uint8_t* __restrict__ out,
+                                                              int log2w, int h, int col, uint32_t t0, uint32_t nt,
+                                                              uint32_t off_h) {
+  const uint32_t w = 1u << log2w, nh = w >> h;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nt * nh) return;
+  const uint32_t t = t0 + g / nh, p = g % nh;
+  size_t rec;
+  if (h == 0) rec = col ? (size_t)p * w + t : (size_t)t * w + p;  // leaves: cell (row t, col p) / (row p, col t)
+  else rec = ((size_t)(col ? w + t : t)) * nh + p;                // levels: [tree][n], rows then columns
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(recs + rec * CDA_REC_BYTES);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(out + ((size_t)(t - t0) * (2 * w - 1) + off_h + p) * CDA_NODE_SIZE);
+#pragma unroll
+  for (int q = 0; q < CDA_NODE_SIZE / 2; q++) dst[q] = src[q];
+}
+
+int launch_pack_tree_level(const void* d_recs, void* d_out, int log2w, int h, bool col, uint32_t t0, uint32_t nt,
+                           uint32_t off_h, hipStream_t s) {
+  const uint32_t n = nt * ((1u << log2w) >> h);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pack_tree_level_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)d_recs,
+                     (uint8_t*)d_out, log2w, h, col ? 1 : 0, t0, nt, off_h);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_merkle_sets(const void* d_recs, const uint32_t* d_idx, const uint32_t* d_off, int nsets, int max_set,
                        void* d_out, void* d_nodes_out, hipStream_t s) {
   if (nsets <= 0) return 0;
