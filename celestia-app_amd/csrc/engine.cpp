@@ -663,15 +663,8 @@ int cda_commit_eds(cda_ctx* c, uint32_t k, const uint8_t* eds, uint8_t* row_root
     if (launch_leaf_hash((const uint8_t*)c->eds.p, c->leaf.p, (unsigned long long*)c->status.p, (int)k, 1, s))
       return CDA_E_DEVICE;
   }
-  {
-    const int lr = launch_nmt_trees(c->leaf.p, c->scratch.p, c->roots.p, (int)k, 1, s, c);
-    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
-  }
-  {
-    ProfScope ps(c, "dah", s);
-    const int lr = launch_dah(c->roots.p, c->dah.p, (int)(2 * w), 1, s);
-    if (lr) return lr == -2 ? CDA_E_UNSUPPORTED : CDA_E_DEVICE;
-  }
+  // trees + DAH as the block path runs one block (the one-launch LDS tree kernel for k <= 128)
+  if ((rc = enqueue_trees(c, k, 1, c->roots.p, c->dah.p, s, 0))) return rc;
   std::vector<uint8_t> recs(roots_b);
   uint64_t st = 0;
   if (!dev_ok(c, hipMemcpyAsync(recs.data(), c->roots.p, roots_b, hipMemcpyDeviceToHost, s), "D2H") ||
