@@ -63,6 +63,21 @@ def test_merkle_roots_vs_oracle(ctx, n):
     assert got[3] == O.sha256(b"")
 
 
+@pytest.mark.parametrize("rows,cols", [(False, True), (True, False)])
+def test_extend_commit_nodes_one_kind(ctx, rows, cols):
+    """Only the column trees, or only the row trees, exported (the device-packed node lists of one kind)."""
+    k = 8
+    ods = O.gen_ods(k, 0xAC)
+    out = ctx.extend_commit_nodes(ods, rows=rows, cols=cols, dah_tree=False)
+    eds_o = O.extend(ods)
+    for axis, key, want in ((0, "row_nodes", rows), (1, "col_nodes", cols)):
+        if not want:
+            assert out[key] is None
+            continue
+        for t in range(2 * k):
+            assert np.array_equal(out[key][t], O.tree_levels(O.axis_leaf_nodes(eds_o, axis, t))), (axis, t)
+
+
 @pytest.mark.parametrize("k", [1, 2, 4, 8, 32])
 def test_extend_commit_nodes_vs_oracle(ctx, k):
     ods = O.gen_ods(k, 0xAB + k)
