@@ -142,8 +142,43 @@ __global__ void __launch_bounds__(256) rs_encode8_kernel(Rs8Args a) {
     s_cb = reinterpret_cast<unsigned long long*>(st + 8 * (a.m << a.log2U));
     for (int i = threadIdx.x; i < 256; i += blockDim.x) s_cb[i] = c_col8[c_skew8[i]];
   }
-  // load + bit-slice: element (s, u), s < m
-  for (int e = threadIdx.x; e < (a.m << a.log2U); e += blockDim.x) {
+  // load + bit-slice: element (s, u), s < m.  At most two elements per thread (the latency launches, whose shards may
+  // sit in page-locked host memory read over PCIe): both loads are issued before either is used, one round trip.
+  const int items = a.m << a.log2U;
+  if (items <= 2 * (int)blockDim.x) {
+    uint4 v[2][2];
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+      const int e = threadIdx.x + it * blockDim.x, s = e >> a.log2U, u = e & (U - 1);
+      if (e < items && s < a.k) {
+        const uint4* p = reinterpret_cast<const uint4*>(src + s * a.src_sh + u * 32);
+        v[it][0] = p[0];
+        v[it][1] = p[1];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+      const int e = threadIdx.x + it * blockDim.x, s = e >> a.log2U, u = e & (U - 1);
+      if (e >= items) continue;
+      uint32_t w[8];
+      if (s < a.k) {
+        if (cpy) {
+          uint4* q = reinterpret_cast<uint4*>(cpy + s * a.cpy_sh + u * 32);
+          q[0] = v[it][0];
+          q[1] = v[it][1];
+        }
+        w[0] = v[it][0].x; w[1] = v[it][0].y; w[2] = v[it][0].z; w[3] = v[it][0].w;
+        w[4] = v[it][1].x; w[5] = v[it][1].y; w[6] = v[it][1].z; w[7] = v[it][1].w;
+        bitslice8(w);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) st[j * items + lds_sw(s * U + u)] = w[j];
+    }
+  }
+  for (int e = threadIdx.x; items > 2 * (int)blockDim.x && e < items; e += blockDim.x) {
     const int s = e >> a.log2U, u = e & (U - 1);
     uint32_t w[8];
     if (s < a.k) {
